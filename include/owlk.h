@@ -1,0 +1,108 @@
+/* libowlk -- MI355X (gfx950) kernels for the owl_wms DiT/MMDiT training hot path.
+ *
+ * C ABI: plain device pointers, int64 sizes/strides (elements), a hipStream_t passed as void*.
+ * Every entry point only enqueues work on `stream`; none allocates, frees or synchronises.
+ * Return value: 0 = ok; 1 = argument error; 2 = HIP launch error.  owlk_last_error() returns a
+ * thread-local message for the last failure.  bf16 buffers are 16-byte aligned with row strides
+ * that are multiples of 8 elements.
+ *
+ * Each entry cites the reference interface it replaces (paths relative to the reference repo).
+ */
+#ifndef OWLK_H
+#define OWLK_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* owlk_last_error(void);
+int owlk_version(void);
+int owlk_device_ok(void);
+
+/* ---- GEMM (replaces every nn.Linear / cuBLAS call on the hot path: attn.py:72-73,82,113;
+ *      mlp.py:29-37; modulation.py:11,32; gamerft.py:26-27; and the X@X.mT / A@A / B@X products
+ *      of muon.py:31-34).
+ *   C[m, n] = epi( sum_k A(m, k) * B(n, k) ),  A(m,k) = a_trans ? A[k*lda+m] : A[m*lda+k],
+ *                                               B(n,k) = b_trans ? B[k*ldb+n] : B[n*ldb+k]
+ *   epi 0 STORE      C = alpha*acc + bf16(bias[n]) + beta*C           (bf16 or fp32 C)
+ *       1 SILU       aux = bf16(acc + bias); C = bf16(silu(aux))
+ *       2 GATE_RESID aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m / tpf, n] * y))
+ *       3 DSILU      C = bf16(bf16(acc) * silu'(aux))
+ *       4 AXPBY      C = bf16(bf16(alpha * bf16(acc)) + bf16(beta * aux))
+ *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes. */
+int owlk_gemm(long M, long N, long K, long batch,
+              const void* A, long lda, long sA, int a_trans,
+              const void* B, long ldb, long sB, int b_trans,
+              void* C, long ldc, long sC, int c_f32,
+              int epi, float alpha, float beta, const float* bias,
+              void* aux, long ldaux, long sAux,
+              const void* gate, long ldgate, long sGate, long tpf,
+              const void* resid, long ldres, long sRes,
+              void* stream);
+
+/* ---- AdaLN modulate (modulation.py:7-26 AdaLN.forward after its fc; :46-55 cond_adaln):
+ *   y[t] = bf16(bf16(bf16(rms_norm(x[t])) * bf16(1 + scale[t/tpf])) + shift[t/tpf]); rstd[t] fp32 */
+int owlk_adaln_fwd(const void* x, long ldx, const void* scale, const void* shift, long ldm, long tpf,
+                   long T, int d, void* y, long ldy, float* rstd, void* yact /* optional bf16(silu(y)),
+                   FinalLayer attn.py:272-277 */, void* stream);
+/* backward: dx = rms_norm' (dy * (1 + scale)) (+ dres); dscale[f] = sum_t dy*xn; dshift[f] = sum_t dy */
+int owlk_adaln_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd,
+                   const void* scale, long ldm, long tpf, long T, int d, const void* dres, long ldres,
+                   void* dx, long lddx, float* dscale, float* dshift, long ldg,
+                   const void* ypre /* optional: dy is d silu(ypre) */, void* stream);
+
+/* ---- Gate backward (modulation.py:28-43 Gate / :57-63 cond_gate; forward is GEMM epi 2):
+ *   dy = bf16(dout * g[t/tpf]); dg[f] = sum_t dout*y; dbias_frames[f] = sum_t dy (optional) */
+int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const void* g, long ldg, long tpf,
+                  long T, int d, void* dy, long lddy, float* dg, float* dbias_frames, long ldr, void* stream);
+
+/* ---- QK RMSNorm + RoPE (attn.py:83-89, rope.py:43-51): qkv rows [q(h d)|k(h d)|v(h d)] ->
+ *   out rows [rope(bf16(rms(q)))|rope(bf16(rms(k)))], rotation pairs (2i, 2i+1) written to
+ *   (i, D/2 + i); cos/sin fp32 tables [*, D/2] at row tab_off + (tpos_div ? t % tpos_div : t). */
+int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const float* cosb, const float* sinb,
+                     long ld_tab, long tab_off, long tpos_div, void* out, long ldo, float* rstd, void* stream);
+int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
+                     const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
+                     const float* rstd, void* dqkv, long ldg, void* stream);
+
+/* ---- Frame-masked flash attention (replaces compiled flex_attention + create_block_mask,
+ *   attn.py:13-16,24-62,106-109; mmattn.py:75).  q/k/v/o token-major rows (head h at column
+ *   h*head_dim), lse [B, H, Lq] natural-log.  Mask: frame = (token + q_offset) / tpf for queries,
+ *   token / tpf for keys; causal; |fq - fk| < window (window <= 0: unlimited); doc[b, fq] ==
+ *   doc[b, fk].  Frame helper arrays (int32 [B, n_frames], batch stride fstride, may be NULL
+ *   without docs): kv_lo (first visible kv frame), q_hi (last query frame seeing a kv frame),
+ *   run_start (first frame of the contiguous same-doc run). */
+int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                  long ldv, long svb, void* o, long ldo, long sob, float* lse, long B, int H, long Lq,
+                  long Lkv, int head_dim, float scale, long tpf, int window, int causal, long q_offset,
+                  const int* kv_lo, const int* q_hi, const int* run_start, const int* doc, long fstride,
+                  void* stream);
+/* delta[b, h, t] = sum_d dO * O (fp32), the backward's row constant */
+int owlk_attn_delta(const void* o, const void* dout, long ld, long B, long L, int H, int D, float* delta,
+                    void* stream);
+int owlk_attn_bwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                  long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
+                  const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb,
+                  void* dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim,
+                  float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
+                  const int* run_start, const int* doc, long fstride, void* stream);
+
+/* ---- Flow-matching noise + patchify (gamerft.py:92-95,107-108,52): x, z [BN, C, P] bf16,
+ *   ts_raw [BN] fp32 (bf16-valued randn) -> xt, tgt token-major [BN*P, C]; ts_out = bf16 sigmoid */
+int owlk_flow_noise(const void* x, const void* z, const float* ts_raw, int C, int P, long BN, void* xt,
+                    void* tgt, float* ts_out, void* stream);
+/* token-major [BN*P, C] -> [BN, C, P] (gamerft.py:58) */
+int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out, void* stream);
+/* MSE (gamerft.py:111): partial[block] = sum (pred - tgt)^2; dpred = bf16(gscale * (pred - tgt)) */
+int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,
+             int nblocks, void* stream);
+/* out[n] += sum_r x[r, n] (bias gradients); x bf16 (x_f32 = 0) or fp32 */
+int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream);
+
+/* ---- Newton-Schulz (muon.py:11-38) helpers: X /= (||X||_F + eps) per batch item, bf16 */
+int owlk_ns_normalize(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
+                      float* work, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,341 @@
+// Block-sparse frame-causal flash attention, backward (gfx950, head_dim 64).
+//
+// Gradient of the reference's flex_attention (attn.py:106-109; autograd of torch's flex
+// template): with P recomputed from the forward log-sum-exp,
+//   dV = P^T dO,  dS = P o (dP - delta),  dP = dO V^T,  delta = rowsum(dO o O),
+//   dK = scale * dS^T Q,  dQ = scale * dS K.
+// Two deterministic kernels (no float atomics):
+//   dkdv : workgroup = 4 waves x 32 keys; sweeps 64-query tiles; S, dP with the key on the lane
+//          (Q/dO rows x K/V in registers), then dV^T += dO^T P and dK^T += Q^T dS take P / dS
+//          straight from the accumulators as B operands.
+//   dq   : workgroup = 4 waves x 32 queries; sweeps 64-key tiles like the forward (query on the
+//          lane), dQ^T += K^T dS^T with K^T fragments through ds_read_b64_tr_b16.
+#include "attn_common.hpp"
+
+namespace {
+
+constexpr int D = 64;
+constexpr int TB = 128;  // rows owned by a workgroup
+constexpr int TL = 64;   // rows per swept tile
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct BwdP {
+  const bf16 *q, *k, *v, *dout;
+  const float *lse, *delta;  // [B, H, Lq]
+  bf16 *dq, *dk, *dv;
+  long ldq, ldk, ldv, ldo, lddq, lddk, lddv;  // token row strides
+  long sqb, skb, svb, sob, sdqb, sdkb, sdvb;  // batch strides
+  long Lq, Lkv;
+  int H;
+  float scale, scale_log2;
+  MaskP m;
+};
+
+DEV void store_rowT(bf16* dst, const f32x16 (&acc)[2], float mul, int h) {
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      bf16x4 v4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = (bf16)(acc[db][4 * gq + e] * mul);
+      *(bf16x4*)(dst + 32 * db + 8 * gq + 4 * h) = v4;
+    }
+}
+
+// ======================================================================== dK, dV
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_k(BwdP p) {
+  constexpr int TILE = TL * D * 2;                     // 8 KiB
+  constexpr int BUF = 2 * TILE + 2 * TL * 4;           // Q | dO | lse2 | delta
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ int red_hi;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, ql = lane & 31;
+  const long b = blockIdx.z;
+  const int head = blockIdx.y;
+  const long k0 = (long)blockIdx.x * TB;
+  const long kw0 = k0 + 32 * w;
+  const MaskP& m = p.m;
+
+  const bf16* Q = p.q + b * p.sqb + head * D;
+  const bf16* K = p.k + b * p.skb + head * D;
+  const bf16* V = p.v + b * p.svb + head * D;
+  const bf16* dO = p.dout + b * p.sob + head * D;
+  const float* LSE = p.lse + (b * p.H + head) * p.Lq;
+  const float* DLT = p.delta + (b * p.H + head) * p.Lq;
+
+  // ---- query range that can see this key block
+  const long klast = (k0 + TB < p.Lkv ? k0 + TB : p.Lkv) - 1;
+  const int fk_lo = frame_of(m, k0), fk_hi = frame_of(m, klast);
+  int fq_end;
+  if (m.q_hi) {
+    if (threadIdx.x == 0) red_hi = -1;
+    __syncthreads();
+    int mx = -1;
+    for (int f = fk_lo + threadIdx.x; f <= fk_hi; f += 256) mx = max(mx, m.q_hi[b * m.fstride + f]);
+    atomicMax(&red_hi, mx);
+    __syncthreads();
+    fq_end = red_hi;
+  } else {
+    fq_end = m.window > 0 ? min(m.n_frames - 1, fk_hi + m.window - 1) : m.n_frames - 1;
+  }
+  const int fq_start = m.causal ? fk_lo : (m.window > 0 ? max(0, fk_lo - m.window + 1) : 0);
+  long qbeg = ((long)fq_start * m.tpf / TL) * TL;
+  long qend = ((long)fq_end + 1) * m.tpf;
+  if (qend > p.Lq) qend = p.Lq;
+  const int ntiles = qend > qbeg ? (int)((qend - qbeg + TL - 1) / TL) : 0;
+
+  // ---- this wave's K and V as B operands (key on the lane): X[key][16 s + 8 h ..]
+  const long my_k = kw0 + ql;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = my_k < p.Lkv ? *(const bf16x8*)(K + my_k * p.ldk + 16 * s + 8 * h) : bf16x8{};
+    vf[s] = my_k < p.Lkv ? *(const bf16x8*)(V + my_k * p.ldv + 16 * s + 8 * h) : bf16x8{};
+  }
+  const bool wave_live = kw0 < p.Lkv;
+  const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
+  const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
+  const int my_fk = frame_of(m, my_k < p.Lkv ? my_k : wklast);
+
+  f32x16 dk[2], dv[2];
+  dk[0] = dk[1] = dv[0] = dv[1] = f32x16{};
+
+  bf16x8 qr[2], dr[2];
+  float lr = 0.f, dl = 0.f;
+  auto load = [&](long q0) {
+    tile_load(qr, Q, p.ldq, q0, p.Lq);
+    tile_load(dr, dO, p.ldo, q0, p.Lq);
+    if (threadIdx.x < TL) {
+      const long qi = q0 + threadIdx.x;
+      lr = qi < p.Lq ? LSE[qi] * LOG2E : 0.f;
+      dl = qi < p.Lq ? DLT[qi] : 0.f;
+    }
+  };
+  auto store = [&](char* buf) {
+    tile_store<SW_DUAL>(buf, qr);
+    tile_store<SW_DUAL>(buf + TILE, dr);
+    if (threadIdx.x < TL) {
+      ((float*)(buf + 2 * TILE))[threadIdx.x] = lr;
+      ((float*)(buf + 2 * TILE + TL * 4))[threadIdx.x] = dl;
+    }
+  };
+  if (ntiles > 0) {
+    load(qbeg);
+    store(smem);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const long q0 = qbeg + (long)t * TL;
+    const bool more = t + 1 < ntiles;
+    if (more) load(q0 + TL);
+    const char* lq = smem + (t & 1) * BUF;
+    const char* ld = lq + TILE;
+    const float* l2 = (const float*)(lq + 2 * TILE);
+    const float* dlt = (const float*)(lq + 2 * TILE + TL * 4);
+
+    const long qlast = (q0 + TL - 1 < p.Lq ? q0 + TL - 1 : p.Lq - 1);
+    int kind = TILE_EMPTY;
+    if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
+    if (kind == TILE_FULL && (q0 + TL > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
+
+    if (kind != TILE_EMPTY) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x16 st = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq, 32 * qb, s, lane), kf[s], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(ld, 32 * qb, s, lane), vf[s], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int rowb = 32 * qb + 8 * g4 + 4 * h;  // rows acc_row(4 g4 + e, h) = rowb + e
+          const f32x4 L = *(const f32x4*)(l2 + rowb);
+          const f32x4 Dl = *(const f32x4*)(dlt + rowb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            float pv = __builtin_amdgcn_exp2f(st[r] * p.scale_log2 - L[e]);
+            if (kind == TILE_PARTIAL) {
+              const long qi = q0 + rowb + e;
+              if (qi >= p.Lq || my_k >= p.Lkv || !allowed(m, b, frame_of(m, qi + m.q_offset), my_fk)) pv = 0.f;
+            }
+            st[r] = pv;
+            dp[r] = pv * (dp[r] - Dl[e]);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = acc_frag(st, s), sf = acc_frag(dp, s);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(ld, 32 * qb, s, db, lane), pf, dv[db],
+                                                             0, 0, 0);
+            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(lq, 32 * qb, s, db, lane), sf, dk[db],
+                                                             0, 0, 0);
+          }
+        }
+      }
+    }
+    if (more) store(smem + ((t + 1) & 1) * BUF);
+    __syncthreads();
+  }
+
+  if (my_k < p.Lkv) {
+    store_rowT(p.dk + b * p.sdkb + my_k * p.lddk + head * D, dk, p.scale, h);
+    store_rowT(p.dv + b * p.sdvb + my_k * p.lddv + head * D, dv, 1.f, h);
+  }
+}
+
+// ======================================================================== dQ
+__global__ __launch_bounds__(256) void attn_bwd_dq_k(BwdP p) {
+  constexpr int TILE = TL * D * 2;
+  constexpr int BUF = 2 * TILE;  // K | V
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ int red_lo;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, ql = lane & 31;
+  const long b = blockIdx.z;
+  const int head = blockIdx.y;
+  const int ntq = (int)((p.Lq + TB - 1) / TB);
+  const long q0 = (long)(ntq - 1 - (int)blockIdx.x) * TB;
+  const long r0 = q0 + 32 * w;
+  const MaskP& m = p.m;
+
+  const bf16* Q = p.q + b * p.sqb + head * D;
+  const bf16* K = p.k + b * p.skb + head * D;
+  const bf16* V = p.v + b * p.svb + head * D;
+  const bf16* dO = p.dout + b * p.sob + head * D;
+
+  const long qlast = (q0 + TB < p.Lq ? q0 + TB : p.Lq) - 1;
+  const int fq_lo = frame_of(m, q0 + m.q_offset), fq_hi = frame_of(m, qlast + m.q_offset);
+  int lo_f;
+  if (m.kv_lo) {
+    if (threadIdx.x == 0) red_lo = 1 << 30;
+    __syncthreads();
+    int mn = 1 << 30;
+    for (int f = fq_lo + threadIdx.x; f <= fq_hi; f += 256) mn = min(mn, m.kv_lo[b * m.fstride + f]);
+    atomicMin(&red_lo, mn);
+    __syncthreads();
+    lo_f = red_lo;
+  } else {
+    lo_f = m.window > 0 ? max(0, fq_lo - m.window + 1) : 0;
+  }
+  const int hi_f = m.causal ? fq_hi : (m.window > 0 ? min(m.n_frames - 1, fq_hi + m.window - 1) : m.n_frames - 1);
+  long kv_begin = ((long)lo_f * m.tpf / TL) * TL;
+  long kv_end = ((long)hi_f + 1) * m.tpf;
+  if (kv_end > p.Lkv) kv_end = p.Lkv;
+  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + TL - 1) / TL) : 0;
+
+  const long my_q = r0 + ql;
+  const bool qok = my_q < p.Lq;
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = qok ? *(const bf16x8*)(Q + my_q * p.ldq + 16 * s + 8 * h) : bf16x8{};
+    df[s] = qok ? *(const bf16x8*)(dO + my_q * p.ldo + 16 * s + 8 * h) : bf16x8{};
+  }
+  const float L2 = qok ? p.lse[(b * p.H + head) * p.Lq + my_q] * LOG2E : 0.f;
+  const float Dl = qok ? p.delta[(b * p.H + head) * p.Lq + my_q] : 0.f;
+  const bool wave_live = r0 < p.Lq;
+  const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
+  const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
+  const int my_fq = frame_of(m, (qok ? my_q : wlast) + m.q_offset);
+
+  f32x16 dq[2];
+  dq[0] = dq[1] = f32x16{};
+  bf16x8 kr[2], vr[2];
+  if (ntiles > 0) {
+    tile_load(kr, K, p.ldk, kv_begin, p.Lkv);
+    tile_load(vr, V, p.ldv, kv_begin, p.Lkv);
+    tile_store<SW_DUAL>(smem, kr);
+    tile_store<SW_ROW>(smem + TILE, vr);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const long c0 = kv_begin + (long)t * TL;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      tile_load(kr, K, p.ldk, c0 + TL, p.Lkv);
+      tile_load(vr, V, p.ldv, c0 + TL, p.Lkv);
+    }
+    const char* lk = smem + (t & 1) * BUF;
+    const char* lv = lk + TILE;
+    const long clast = (c0 + TL - 1 < p.Lkv ? c0 + TL - 1 : p.Lkv - 1);
+    int kind = TILE_EMPTY;
+    if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
+    if (kind == TILE_FULL && c0 + TL > p.Lkv) kind = TILE_PARTIAL;
+
+    if (kind != TILE_EMPTY) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x16 st = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lk, 32 * kb, s, lane), qf[s], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_ROW>(lv, 32 * kb, s, lane), df[s], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pv = __builtin_amdgcn_exp2f(st[r] * p.scale_log2 - L2);
+          if (kind == TILE_PARTIAL) {
+            const long key = c0 + 32 * kb + acc_row(r, h);
+            if (key >= p.Lkv || !qok || !allowed(m, b, my_fq, frame_of(m, key))) pv = 0.f;
+          }
+          dp[r] = pv * (dp[r] - Dl);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 sf = acc_frag(dp, s);
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(lk, 32 * kb, s, db, lane), sf, dq[db],
+                                                             0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      char* nb = smem + ((t + 1) & 1) * BUF;
+      tile_store<SW_DUAL>(nb, kr);
+      tile_store<SW_ROW>(nb + TILE, vr);
+    }
+    __syncthreads();
+  }
+  if (qok) store_rowT(p.dq + b * p.sdqb + my_q * p.lddq + head * D, dq, p.scale, h);
+}
+
+}  // namespace
+
+extern "C" int owlk_attn_bwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                             long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
+                             const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb,
+                             void* dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim,
+                             float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
+                             const int* run_start, const int* doc, long fstride, void* stream) {
+  OWLK_REQUIRE(head_dim == D, "attn_bwd: head_dim %d not built (64 only)", head_dim);
+  OWLK_REQUIRE(tpf > 0 && Lq > 0 && Lkv > 0 && B > 0 && H > 0 && Lq == Lkv, "attn_bwd: training shapes only");
+  OWLK_REQUIRE(!doc || run_start, "attn_bwd: doc mask needs run_start");
+  OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)dout | (uintptr_t)dq | (uintptr_t)dk |
+                (uintptr_t)dv) % 16 == 0,
+               "attn_bwd: operands must be 16-byte aligned");
+  BwdP p;
+  p.q = (const bf16*)q; p.k = (const bf16*)k; p.v = (const bf16*)v; p.dout = (const bf16*)dout;
+  p.lse = lse; p.delta = delta;
+  p.dq = (bf16*)dq; p.dk = (bf16*)dk; p.dv = (bf16*)dv;
+  p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo; p.lddq = lddq; p.lddk = lddk; p.lddv = lddv;
+  p.sqb = sqb; p.skb = skb; p.svb = svb; p.sob = sob; p.sdqb = sdqb; p.sdkb = sdkb; p.sdvb = sdvb;
+  p.Lq = Lq; p.Lkv = Lkv; p.H = H;
+  p.scale = scale;
+  p.scale_log2 = scale * LOG2E;
+  p.m = owlk_make_mask(tpf, window, causal, 0, Lkv, kv_lo, q_hi, run_start, doc, fstride);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256), 0,
+                     s, p);
+  if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
+  hipLaunchKernelGGL(attn_bwd_dq_k, dim3((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256), 0, s,
+                     p);
+  return owlk::check_launch("attn_bwd_dq");
+}

@@ -1,0 +1,141 @@
+// Frame-mask geometry shared by the attention kernels.
+//
+// Reference mask (attn.py:24-62, mask_mod):  allowed(q, kv) <=>
+//     frame_kv <= frame_q                         (causal)
+//   & |frame_q - frame_kv| < window               (window_len; None = all frames)
+//   & doc_id[b, frame_q] == doc_id[b, frame_kv]   (packed documents)
+// with frame(i) = i // tokens_per_frame and q shifted by q_offset (KV-cache decode).
+// Nothing is materialised: tiles are classified EMPTY / FULL / PARTIAL from frame ranges and
+// per-frame helper arrays built once per forward by the host:
+//   kv_lo[b, f]     first kv frame any query of frame f may see (window + first doc occurrence)
+//   q_hi[b, f]      last query frame that may see kv frame f
+//   run_start[b, f] first frame of the contiguous same-doc run holding f
+//   doc[b, f]       doc id (int32)
+#pragma once
+#include "common.hpp"
+
+struct MaskP {
+  long tpf;            // tokens per frame
+  unsigned magic;      // floor(2^32 / tpf) + 1 (exact frame division for idx < 2^32 / tpf); 0 if tpf == 1
+  int window;          // frames; <= 0 means unlimited
+  int causal;
+  long q_offset;       // tokens (KV cache)
+  int n_frames;        // kv frames (Lkv / tpf, rounded up)
+  const int* kv_lo;    // [B, n_frames] or null
+  const int* q_hi;     // [B, n_frames] or null
+  const int* run_start;
+  const int* doc;
+  long fstride;        // batch stride of the frame arrays
+};
+
+DEV int frame_of(const MaskP& m, long idx) {
+  return m.magic ? (int)__umulhi((unsigned)idx, m.magic) : (int)idx;
+}
+
+enum TileKind { TILE_EMPTY = 0, TILE_FULL = 1, TILE_PARTIAL = 2 };
+
+// classify query frames [fq0, fq1] x kv frames [fk0, fk1] for batch b
+DEV int classify(const MaskP& m, long b, int fq0, int fq1, int fk0, int fk1) {
+  if (m.causal && fk0 > fq1) return TILE_EMPTY;
+  if (m.window > 0) {
+    if (fq0 - fk1 >= m.window) return TILE_EMPTY;
+    if (!m.causal && fk0 - fq1 >= m.window) return TILE_EMPTY;
+  }
+  bool pure_doc = true;
+  if (m.doc) {
+    const int* rs = m.run_start + b * m.fstride;
+    const int* dc = m.doc + b * m.fstride;
+    const int lo = fq0 < fk0 ? fq0 : fk0, hi = fq1 > fk1 ? fq1 : fk1;
+    pure_doc = rs[hi] <= lo;
+    if (!pure_doc && rs[fq1] <= fq0 && rs[fk1] <= fk0 && dc[fq0] != dc[fk0]) return TILE_EMPTY;
+  }
+  bool full = pure_doc;
+  if (m.causal) full = full && fk1 <= fq0;
+  if (m.window > 0) {
+    full = full && (fq1 - fk0 < m.window);
+    if (!m.causal) full = full && (fk1 - fq0 < m.window);
+  }
+  return full ? TILE_FULL : TILE_PARTIAL;
+}
+
+DEV bool allowed(const MaskP& m, long b, int fq, int fk) {
+  if (m.causal && fk > fq) return false;
+  if (m.window > 0) {
+    const int dd = fq > fk ? fq - fk : fk - fq;
+    if (dd >= m.window) return false;
+  }
+  if (m.doc) {
+    const int* dc = m.doc + b * m.fstride;
+    if (dc[fq] != dc[fk]) return false;
+  }
+  return true;
+}
+
+// 128-B-row (64 x bf16) tile swizzles: K is read row-wise (ds_read_b128), V through
+// ds_read_b64_tr_b16; each gets its own conflict-free XOR of the 16-B chunk index.
+DEV int swz_row(int r) { return (r >> 1) & 7; }
+DEV int swz_tr(int r) { return ((r >> 1) & 1) << 2; }
+// one image serving both row reads (32x32x16 A operand) and transposed reads: distinct chunk
+// XORs among same-parity rows of every ds_read_b128 lane group, bit 2 flipping between row
+// pairs (r, r+2) for the tr_b16 half-waves.
+DEV int swz_dual(int r) { return ((r >> 1) & 7) ^ (((r >> 1) & 1) << 2); }
+
+enum Swz { SW_ROW = 0, SW_TR = 1, SW_DUAL = 2 };
+template <int S>
+DEV int swz(int r) {
+  return S == SW_ROW ? swz_row(r) : (S == SW_TR ? swz_tr(r) : swz_dual(r));
+}
+
+// 64 rows x 64 bf16 (128-B rows) tile: global -> 2 x 16 B per thread (256 threads) -> LDS
+DEV void tile_load(bf16x8 (&r)[2], const bf16* base, long ld, long r0, long R) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const long row = r0 + (c >> 3);
+    r[i] = (row >= 0 && row < R) ? *(const bf16x8*)(base + row * ld + (c & 7) * 8) : bf16x8{};
+  }
+}
+
+template <int S>
+DEV void tile_store(char* lds, const bf16x8 (&r)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int row = c >> 3, ch = c & 7;
+    *(bf16x8*)(lds + row * 128 + ((ch ^ swz<S>(row)) << 4)) = r[i];
+  }
+}
+
+// A/B fragment of v_mfma_f32_32x32x16_bf16 read row-wise: rows row0 + (lane & 31), k = 16 s + 8 h
+template <int S>
+DEV bf16x8 frag_row(const char* lds, int row0, int s, int lane) {
+  const int r = row0 + (lane & 31);
+  return *(const bf16x8*)(lds + r * 128 + (((2 * s + (lane >> 5)) ^ swz<S>(r)) << 4));
+}
+
+// A fragment X^T-ordered for a product that consumes an accumulator tile as its B operand:
+// lane (col = 32 cb + (lane & 31), half h) element j <- tile[row0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)][col]
+template <int S>
+DEV bf16x8 frag_tr(const char* lds, int row0, int s, int cb, int lane) {
+  const int g = lane >> 4, h = lane >> 5;
+  const int qq = (lane & 15) >> 2, pp = lane & 3;
+  const int ra = row0 + 16 * s + 4 * h + qq, rb_ = ra + 8;
+  const int ch = 4 * cb + 2 * (g & 1) + (pp >> 1);
+  const s16x4 lo = ds_read_tr16(lds + ra * 128 + ((ch ^ swz<S>(ra)) << 4) + 8 * (pp & 1));
+  const s16x4 hi = ds_read_tr16(lds + rb_ * 128 + ((ch ^ swz<S>(rb_)) << 4) + 8 * (pp & 1));
+  return join_tr(lo, hi);
+}
+
+// accumulator registers 8 s .. 8 s + 7 of a 32x32 tile -> bf16 B fragment for k-step s
+DEV bf16x8 acc_frag(const f32x16& a, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (bf16)a[8 * s + j];
+  return f;
+}
+
+// row (register) index -> row of a 32x32 accumulator tile for lane half h
+DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+MaskP owlk_make_mask(long tpf, int window, int causal, long q_offset, long Lkv, const int* kv_lo, const int* q_hi,
+                     const int* run_start, const int* doc, long fstride);

@@ -1,0 +1,269 @@
+// Block-sparse frame-causal flash attention, forward (gfx950, head_dim 64).
+//
+// Replaces the compiled flex_attention + create_block_mask pair of the reference
+// (attn.py:13-16, 24-62, 106-109; mmattn.py:75).  Semantics: softmax(q k^T / sqrt(D)) v over the
+// allowed keys of attn_common.hpp, bf16 in / fp32 accumulate / bf16 out, plus the per-row
+// log-sum-exp (natural log) for the backward pass.
+//
+// Workgroup = 4 waves = 128 query rows of one (batch, head); each wave owns 32 rows.  Per 64-key
+// tile the wave computes S^T = K Q^T with v_mfma_f32_32x32x16_bf16 (key rows in registers, the
+// query on the lane) so the softmax row statistics stay in-lane (+ one lane^32 exchange), then
+// feeds the S^T accumulators straight back as the B operand of O^T += V^T P^T (V^T fragments
+// through ds_read_b64_tr_b16).  K/V tiles are register-staged into a double-buffered LDS ring.
+#include "attn_common.hpp"
+
+namespace {
+
+constexpr int D = 64;
+constexpr int QT = 128;  // query rows per workgroup
+constexpr int KT = 64;   // keys per tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+struct FwdP {
+  const bf16 *q, *k, *v;
+  bf16* o;
+  float* lse;           // [B, H, Lq]
+  long ldq, ldk, ldv, ldo;      // token row strides (elements)
+  long sqb, skb, svb, sob;      // batch strides (elements)
+  long Lq, Lkv;
+  int H;
+  float scale_log2;     // softmax scale * log2(e)
+  MaskP m;
+};
+
+// stage one 64x64 bf16 tile (rows r0.., 128-B rows) into registers: 2 chunks per thread
+DEV void stage_load(bf16x8 (&r)[2], const bf16* base, long ld, long r0, long R) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const long row = r0 + (c >> 3);
+    r[i] = row < R ? *(const bf16x8*)(base + row * ld + (c & 7) * 8) : bf16x8{};
+  }
+}
+
+template <bool TR>
+DEV void stage_store(char* lds, const bf16x8 (&r)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int row = c >> 3, ch = c & 7;
+    const int sw = TR ? swz_tr(row) : swz_row(row);
+    *(bf16x8*)(lds + row * 128 + ((ch ^ sw) << 4)) = r[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * KT * D * 2];  // [buf][K|V][64][64]
+  __shared__ int red_lo;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, ql = lane & 31;
+  const long b = blockIdx.z;
+  const int head = blockIdx.y;
+  const int ntq = (int)((p.Lq + QT - 1) / QT);
+  const long q0 = (long)(ntq - 1 - (int)blockIdx.x) * QT;  // heaviest (latest) query tiles first
+  const long r0 = q0 + 32 * w;                             // this wave's first row
+  const MaskP& m = p.m;
+
+  const bf16* Q = p.q + b * p.sqb + head * D;
+  const bf16* K = p.k + b * p.skb + head * D;
+  const bf16* V = p.v + b * p.svb + head * D;
+
+  // ---- kv frame range of the whole workgroup
+  const long qlast = (q0 + QT < p.Lq ? q0 + QT : p.Lq) - 1;
+  const int fq_lo = frame_of(m, q0 + m.q_offset), fq_hi = frame_of(m, qlast + m.q_offset);
+  int lo_f;
+  if (m.kv_lo) {
+    if (threadIdx.x == 0) red_lo = 1 << 30;
+    __syncthreads();
+    int mn = 1 << 30;
+    for (int f = fq_lo + threadIdx.x; f <= fq_hi; f += 256) mn = min(mn, m.kv_lo[b * m.fstride + f]);
+    atomicMin(&red_lo, mn);
+    __syncthreads();
+    lo_f = red_lo;
+  } else {
+    lo_f = m.window > 0 ? max(0, fq_lo - m.window + 1) : 0;
+  }
+  int hi_f = m.causal ? fq_hi : (m.window > 0 ? min(m.n_frames - 1, fq_hi + m.window - 1) : m.n_frames - 1);
+  long kv_begin = (long)lo_f * m.tpf;
+  long kv_end = ((long)hi_f + 1) * m.tpf;
+  if (kv_end > p.Lkv) kv_end = p.Lkv;
+  kv_begin = (kv_begin / KT) * KT;
+  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + KT - 1) / KT) : 0;
+
+  // ---- this wave's query fragments (B operand of S^T = K Q^T): Q[row][16s + 8h .. +8]
+  const long my_q = r0 + ql;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    qf[s] = my_q < p.Lq ? *(const bf16x8*)(Q + my_q * p.ldq + 16 * s + 8 * h) : bf16x8{};
+  const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
+  const bool wave_live = r0 < p.Lq;
+  const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
+  const int my_fq = frame_of(m, (my_q < p.Lq ? my_q : wlast) + m.q_offset);
+
+  f32x16 o[2];
+  o[0] = f32x16{};
+  o[1] = f32x16{};
+  float mrow = -INFINITY, lrow = 0.f;
+
+  bf16x8 kr[2], vr[2];
+  if (ntiles > 0) {
+    stage_load(kr, K, p.ldk, kv_begin, p.Lkv);
+    stage_load(vr, V, p.ldv, kv_begin, p.Lkv);
+    stage_store<false>(smem, kr);
+    stage_store<true>(smem + KT * D * 2, vr);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const long c0 = kv_begin + (long)t * KT;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(kr, K, p.ldk, c0 + KT, p.Lkv);
+      stage_load(vr, V, p.ldv, c0 + KT, p.Lkv);
+    }
+    const char* lk = smem + (t & 1) * (2 * KT * D * 2);
+    const char* lv = lk + KT * D * 2;
+
+    const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
+    int kind = TILE_EMPTY;
+    if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
+    if (kind == TILE_FULL && c0 + KT > p.Lkv) kind = TILE_PARTIAL;
+
+    if (kind != TILE_EMPTY) {
+      // S^T[key][q] for two 32-key blocks
+      f32x16 st[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        st[kb] = f32x16{};
+        const int krow = 32 * kb + ql;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = *(const bf16x8*)(lk + krow * 128 + (((2 * s + h) ^ swz_row(krow)) << 4));
+          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[kb], 0, 0, 0);
+        }
+      }
+      // mask + scale into the log2 domain
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float sv = st[kb][r] * p.scale_log2;
+          if (kind == TILE_PARTIAL) {
+            const long key = c0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key >= p.Lkv || my_q >= p.Lq || !allowed(m, b, my_fq, frame_of(m, key))) sv = -INFINITY;
+          }
+          st[kb][r] = sv;
+          tmax = fmaxf(tmax, sv);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(mrow, tmax);
+      const float msafe = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = __builtin_amdgcn_exp2f(mrow - msafe);
+      mrow = mnew;
+      float psum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(st[kb][r] - msafe);
+          st[kb][r] = pv;
+          psum += pv;
+        }
+      lrow = lrow * alpha + psum;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+
+      // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf[j] = (bf16)st[kb][8 * s + j];
+          const int g = lane >> 4;
+          const int qq = (lane & 15) >> 2, pp = lane & 3;
+          const int rowa = 32 * kb + 16 * s + 4 * h + qq;
+          const int rowb = rowa + 8;
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const int ch = 4 * db + 2 * (g & 1) + (pp >> 1);
+            const s16x4 lo = ds_read_tr16(lv + rowa * 128 + ((ch ^ swz_tr(rowa)) << 4) + 8 * (pp & 1));
+            const s16x4 hi = ds_read_tr16(lv + rowb * 128 + ((ch ^ swz_tr(rowb)) << 4) + 8 * (pp & 1));
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(join_tr(lo, hi), pf, o[db], 0, 0, 0);
+          }
+        }
+    }
+    if (more) {
+      char* nb = smem + ((t + 1) & 1) * (2 * KT * D * 2);
+      stage_store<false>(nb, kr);
+      stage_store<true>(nb + KT * D * 2, vr);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: O = O^T / l, lse
+  const float ltot = lrow + __shfl_xor(lrow, 32, 64);
+  if (my_q < p.Lq) {
+    const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+    bf16* O = p.o + b * p.sob + my_q * p.ldo + head * D;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        bf16x4 v4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[db][4 * gq + e] * inv);
+        *(bf16x4*)(O + 32 * db + 8 * gq + 4 * h) = v4;
+      }
+    if (h == 0) p.lse[(b * p.H + head) * p.Lq + my_q] = ltot > 0.f ? (mrow + __log2f(ltot)) * LN2 : -INFINITY;
+  }
+}
+
+}  // namespace
+
+MaskP owlk_make_mask(long tpf, int window, int causal, long q_offset, long Lkv, const int* kv_lo, const int* q_hi,
+                     const int* run_start, const int* doc, long fstride) {
+  MaskP m;
+  m.tpf = tpf;
+  m.magic = tpf > 1 ? (unsigned)((1ull << 32) / (unsigned long long)tpf + 1) : 0u;
+  m.window = window;
+  m.causal = causal;
+  m.q_offset = q_offset;
+  m.n_frames = (int)((Lkv + tpf - 1) / tpf);
+  m.kv_lo = kv_lo;
+  m.q_hi = q_hi;
+  m.run_start = run_start;
+  m.doc = doc;
+  m.fstride = fstride;
+  return m;
+}
+
+extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                             long ldv, long svb, void* o, long ldo, long sob, float* lse, long B, int H, long Lq,
+                             long Lkv, int head_dim, float scale, long tpf, int window, int causal, long q_offset,
+                             const int* kv_lo, const int* q_hi, const int* run_start, const int* doc, long fstride,
+                             void* stream) {
+  OWLK_REQUIRE(head_dim == D, "attn_fwd: head_dim %d not built (64 only)", head_dim);
+  OWLK_REQUIRE(tpf > 0 && Lq > 0 && Lkv > 0 && B > 0 && H > 0, "attn_fwd: bad sizes");
+  OWLK_REQUIRE((Lkv + q_offset) < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_fwd: sequence too long");
+  OWLK_REQUIRE(!doc || (run_start != nullptr), "attn_fwd: doc mask needs run_start");
+  OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16 == 0 && ldq % 8 == 0 &&
+                   ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0,
+               "attn_fwd: q/k/v/o rows must be 16-byte aligned");
+  FwdP p;
+  p.q = (const bf16*)q; p.k = (const bf16*)k; p.v = (const bf16*)v; p.o = (bf16*)o; p.lse = lse;
+  p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
+  p.sqb = sqb; p.skb = skb; p.svb = svb; p.sob = sob;
+  p.Lq = Lq; p.Lkv = Lkv; p.H = H;
+  p.scale_log2 = scale * LOG2E;
+  p.m = owlk_make_mask(tpf, window, causal, q_offset, Lkv, kv_lo, q_hi, run_start, doc, fstride);
+  dim3 grid((unsigned)((Lq + QT - 1) / QT), (unsigned)H, (unsigned)B);
+  hipLaunchKernelGGL(attn_fwd_k, grid, dim3(256), 0, (hipStream_t)stream, p);
+  return owlk::check_launch("attn_fwd");
+}

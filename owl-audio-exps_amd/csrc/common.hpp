@@ -1,0 +1,80 @@
+// Shared device helpers for libowlk (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define DEV __device__ __forceinline__
+
+// round-to-nearest-even through bf16, as autocast does after every bf16 op.  Integer form on
+// purpose: hipcc contracts (float)(__bf16)(a*b) + c into an FMA, silently dropping the rounding.
+DEV float rb(float x) {
+  unsigned u = __float_as_uint(x);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return __uint_as_float(u & 0xFFFF0000u);
+}
+DEV float bf2f(bf16 x) { return (float)x; }
+
+DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+// LDS pointer helpers
+typedef s16x4 __attribute__((address_space(3))) * lds_s16x4_ptr;
+
+DEV s16x4 ds_read_tr16(const void* lds_byte_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(lds_byte_ptr));
+}
+
+DEV bf16x8 join_tr(s16x4 lo, s16x4 hi) {
+  union { s16x4 s[2]; bf16x8 v; } u;
+  u.s[0] = lo;
+  u.s[1] = hi;
+  return u.v;
+}
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 8 x bf16 <-> 8 x f32
+DEV void unpack8(const bf16x8& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
+}
+DEV bf16x8 pack8(const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (bf16)f[i];
+  return v;
+}
+
+// ---------------------------------------------------------------- host-side error plumbing
+#ifdef __cplusplus
+#include <cstdio>
+#include <string>
+namespace owlk {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace owlk
+#define OWLK_REQUIRE(cond, ...)             \
+  do {                                      \
+    if (!(cond)) {                          \
+      owlk::set_error(__VA_ARGS__);         \
+      return 1;                             \
+    }                                       \
+  } while (0)
+#endif

@@ -1,0 +1,568 @@
+// HBM-bound fused kernels of the DiT block (gfx950).  Every kernel moves bf16 rows as 16-B
+// chunks (8 elements per lane) and reproduces the reference's bf16 autocast rounding order:
+//   AdaLN      modulation.py:7-26 / cond_adaln :46-55   y = bf16(bf16(bf16(rms(x)) * bf16(1+a)) + b)
+//   Gate       modulation.py:28-43 / cond_gate :57-63   (fwd fused into the GEMM epilogue)
+//   QK-norm    attn.py:84 + rope.py:43-51               fp32 rotation of bf16(rms(q)), [even||odd]
+//   flow noise gamerft.py:92-95,107-111                 x_t = bf16(bf16(x*bf16(1-t)) + bf16(z*t))
+#include "common.hpp"
+
+namespace {
+
+constexpr float RMS_EPS = 1.1920928955078125e-07f;  // finfo(float32).eps, F.rms_norm default
+constexpr int MAXCPL = 8;  // max 16-B chunks per lane (d <= 4096)
+
+// launch helper: pick the chunks-per-lane instantiation for a row width d
+#define OWLK_CPL_DISPATCH(d, KERNEL, ...)                     \
+  do {                                                        \
+    const int cpl_ = ((d) / 8 + 63) / 64;                     \
+    switch (cpl_) {                                           \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break; \
+      case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break; \
+      case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break; \
+      case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break; \
+      case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
+      case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break; \
+      default: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break; \
+    }                                                         \
+  } while (0)
+
+// ------------------------------------------------------------------ AdaLN forward
+// one wave per token row; lane owns chunks c = lane + 64*i
+template <int MAXC>
+__global__ __launch_bounds__(256) void adaln_fwd_k(const bf16* __restrict__ x, long ldx,
+                                                   const bf16* __restrict__ sc, const bf16* __restrict__ sh,
+                                                   long ldm, long tpf, long T, int d, bf16* __restrict__ y,
+                                                   long ldy, float* __restrict__ rstd, bf16* __restrict__ yact) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int nch = d / 8;
+  bf16x8 xv[MAXC];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      xv[i] = *(const bf16x8*)(x + row * ldx + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)xv[i][e];
+        ss += f * f;
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / d + RMS_EPS);
+  if (lane == 0 && rstd) rstd[row] = r;
+  const long f = row / tpf;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      float a[8], b[8], o[8];
+      unpack8(*(const bf16x8*)(sc + f * ldm + c * 8), a);
+      unpack8(*(const bf16x8*)(sh + f * ldm + c * 8), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xn = rb((float)xv[i][e] * r);
+        o[e] = rb(rb(xn * rb(1.f + a[e])) + b[e]);
+      }
+      *(bf16x8*)(y + row * ldy + c * 8) = pack8(o);
+      if (yact) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = silu_f(o[e]);
+        *(bf16x8*)(yact + row * ldy + c * 8) = pack8(o);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ AdaLN backward
+// one workgroup per frame (tpf token rows); wave w takes rows w, w+4, ...; each lane keeps the
+// per-column partial sums of its chunks, combined across the 4 waves through LDS at the end.
+template <int MAXC>
+__global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, long lddy,
+                                                   const bf16* __restrict__ x, long ldx,
+                                                   const float* __restrict__ rstd,
+                                                   const bf16* __restrict__ sc, long ldm, long tpf, int d,
+                                                   const bf16* __restrict__ dres, long ldres,
+                                                   bf16* __restrict__ dx, long lddx,
+                                                   float* __restrict__ dsc, float* __restrict__ dsh, long ldg,
+                                                   const bf16* __restrict__ ypre) {
+  extern __shared__ float red[];  // [4][2][d]
+  const long f = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = d / 8;
+  float pa[MAXC][8], pb[MAXC][8];
+  float t1[MAXC][8];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pa[i][e] = pb[i][e] = 0.f;
+    if (c < nch) {
+      float a[8];
+      unpack8(*(const bf16x8*)(sc + f * ldm + c * 8), a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t1[i][e] = rb(1.f + a[e]);
+    }
+  }
+  for (long t = w; t < tpf; t += 4) {
+    const long row = f * tpf + t;
+    const float r = rstd[row];
+    float g[MAXC][8], xh[MAXC][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float dv[8], xv[8];
+        unpack8(*(const bf16x8*)(dy + row * lddy + c * 8), dv);
+        unpack8(*(const bf16x8*)(x + row * ldx + c * 8), xv);
+        if (ypre) {  // FinalLayer: dy arrives as d silu(y); silu backward in bf16 like autocast
+          float yp[8];
+          unpack8(*(const bf16x8*)(ypre + row * lddy + c * 8), yp);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float sg = 1.f / (1.f + __expf(-yp[e]));
+            dv[e] = rb(dv[e] * sg * (1.f + yp[e] * (1.f - sg)));
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[i][e] = xv[e] * r;
+          const float xn = rb(xh[i][e]);
+          pa[i][e] += dv[e] * xn;
+          pb[i][e] += dv[e];
+          g[i][e] = dv[e] * t1[i][e];
+          dot += g[i][e] * xh[i][e];
+        }
+      }
+    }
+    dot = wave_sum(dot) / d;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[8], rs[8];
+        if (dres) unpack8(*(const bf16x8*)(dres + row * ldres + c * 8), rs);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = r * (g[i][e] - xh[i][e] * dot) + (dres ? rs[e] : 0.f);
+        *(bf16x8*)(dx + row * lddx + c * 8) = pack8(o);
+      }
+    }
+  }
+  // combine the 4 waves' column partials
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(w * 2 + 0) * d + c * 8 + e] = pa[i][e];
+        red[(w * 2 + 1) * d + c * 8 + e] = pb[i][e];
+      }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < d; j += 256) {
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      sa += red[(ww * 2 + 0) * d + j];
+      sb += red[(ww * 2 + 1) * d + j];
+    }
+    dsc[f * ldg + j] = sa;
+    dsh[f * ldg + j] = sb;
+  }
+}
+
+// ------------------------------------------------------------------ Gate backward
+// forward: out = resid + bf16(g[frame] * y)  (fused in the GEMM epilogue)
+// backward: dy = bf16(dout * g); dg[frame] = sum_t dout*y; dyf[frame] = sum_t dy (bias partials)
+template <int MAXC>
+__global__ __launch_bounds__(256) void gate_bwd_k(const bf16* __restrict__ dout, long ldo,
+                                                  const bf16* __restrict__ y, long ldy,
+                                                  const bf16* __restrict__ g, long ldg, long tpf, int d,
+                                                  bf16* __restrict__ dy, long lddy,
+                                                  float* __restrict__ dg, float* __restrict__ dbf, long ldr) {
+  extern __shared__ float red[];
+  const long f = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = d / 8;
+  float pg[MAXC][8], pb[MAXC][8], gv[MAXC][8];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pg[i][e] = pb[i][e] = 0.f;
+    if (c < nch) unpack8(*(const bf16x8*)(g + f * ldg + c * 8), gv[i]);
+  }
+  for (long t = w; t < tpf; t += 4) {
+    const long row = f * tpf + t;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float dv[8], yv[8], o[8];
+        unpack8(*(const bf16x8*)(dout + row * ldo + c * 8), dv);
+        unpack8(*(const bf16x8*)(y + row * ldy + c * 8), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pg[i][e] += dv[e] * yv[e];
+          o[e] = rb(dv[e] * gv[i][e]);
+          pb[i][e] += o[e];
+        }
+        *(bf16x8*)(dy + row * lddy + c * 8) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(w * 2 + 0) * d + c * 8 + e] = pg[i][e];
+        red[(w * 2 + 1) * d + c * 8 + e] = pb[i][e];
+      }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < d; j += 256) {
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      sa += red[(ww * 2 + 0) * d + j];
+      sb += red[(ww * 2 + 1) * d + j];
+    }
+    dg[f * ldr + j] = sa;
+    if (dbf) dbf[f * ldr + j] = sb;
+  }
+}
+
+// ------------------------------------------------------------------ QK RMSNorm + RoPE
+// one (token, q|k, head) row of D = 8*CPR elements per CPR lanes; lane owns 4 rotation pairs.
+// qkv row layout (attn.py:83): [q(h d) | k(h d) | v(h d)]; out row: [q_rot(h d) | k_rot(h d)]
+template <int D>
+__global__ __launch_bounds__(256) void qk_rope_fwd_k(const bf16* __restrict__ qkv, long ldq, long T, int H,
+                                                     const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                     long ld_tab, long tab_off, long tpos_div,
+                                                     bf16* __restrict__ out, long ldo, float* __restrict__ rstd) {
+  constexpr int CPR = D / 8;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rowid = gid / CPR;  // (token, which, head)
+  const int j = gid % CPR;
+  if (rowid >= T * 2 * H) return;
+  const long tok = rowid / (2 * H);
+  const int wh = rowid % (2 * H);  // which*H + head
+  const bf16x8 v = *(const bf16x8*)(qkv + tok * ldq + (long)wh * D + j * 8);
+  float xv[8];
+  unpack8(v, xv);
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ss += xv[e] * xv[e];
+#pragma unroll
+  for (int o = 1; o < CPR; o <<= 1) ss += __shfl_xor(ss, o, 64);
+  const float r = rsqrtf(ss / D + RMS_EPS);
+  if (j == 0 && rstd) rstd[tok * 2 * H + wh] = r;
+  const long pos = tab_off + (tpos_div > 0 ? tok % tpos_div : tok);
+  const f32x4 c = *(const f32x4*)(cosb + pos * ld_tab + j * 4);
+  const f32x4 s = *(const f32x4*)(sinb + pos * ld_tab + j * 4);
+  bf16x4 y0, y1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = rb(xv[2 * i] * r), x1 = rb(xv[2 * i + 1] * r);
+    y0[i] = (bf16)(x0 * c[i] - x1 * s[i]);
+    y1[i] = (bf16)(x1 * c[i] + x0 * s[i]);
+  }
+  bf16* o = out + tok * ldo + (long)wh * D;
+  *(bf16x4*)(o + j * 4) = y0;
+  *(bf16x4*)(o + D / 2 + j * 4) = y1;
+}
+
+// backward: d(q_rot) -> inverse rotation -> rms_norm backward (recomputing xhat from raw qkv)
+template <int D>
+__global__ __launch_bounds__(256) void qk_rope_bwd_k(const bf16* __restrict__ dqk, long ldd,
+                                                     const bf16* __restrict__ qkv, long ldq, long T, int H,
+                                                     const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                     long ld_tab, long tab_off, long tpos_div,
+                                                     const float* __restrict__ rstd,
+                                                     bf16* __restrict__ dqkv, long ldg) {
+  constexpr int CPR = D / 8;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rowid = gid / CPR;
+  const int j = gid % CPR;
+  if (rowid >= T * 2 * H) return;
+  const long tok = rowid / (2 * H);
+  const int wh = rowid % (2 * H);
+  const bf16* dp = dqk + tok * ldd + (long)wh * D;
+  const bf16x4 d0 = *(const bf16x4*)(dp + j * 4);
+  const bf16x4 d1 = *(const bf16x4*)(dp + D / 2 + j * 4);
+  const long pos = tab_off + (tpos_div > 0 ? tok % tpos_div : tok);
+  const f32x4 c = *(const f32x4*)(cosb + pos * ld_tab + j * 4);
+  const f32x4 s = *(const f32x4*)(sinb + pos * ld_tab + j * 4);
+  float dxn[8], xh[8];
+  const float r = rstd[tok * 2 * H + wh];
+  float xv[8];
+  unpack8(*(const bf16x8*)(qkv + tok * ldq + (long)wh * D + j * 8), xv);
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = (float)d0[i], b = (float)d1[i];
+    dxn[2 * i] = a * c[i] + b * s[i];
+    dxn[2 * i + 1] = b * c[i] - a * s[i];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    xh[e] = xv[e] * r;
+    dot += dxn[e] * xh[e];
+  }
+#pragma unroll
+  for (int o = 1; o < CPR; o <<= 1) dot += __shfl_xor(dot, o, 64);
+  dot /= D;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = r * (dxn[e] - xh[e] * dot);
+  *(bf16x8*)(dqkv + tok * ldg + (long)wh * D + j * 8) = pack8(o);
+}
+
+// ------------------------------------------------------------------ flow noise + patchify
+// x, z: [B, N, C, P] (P = h*w pixels); ts_raw: [B, N] fp32 (pre-sigmoid draw, bf16-valued)
+// out: xt_tok, tgt_tok: [B, N*P, C] bf16 token-major (gamerft.py:52 'b n c h w -> b (n h w) c')
+__global__ __launch_bounds__(256) void flow_noise_k(const bf16* __restrict__ x, const bf16* __restrict__ z,
+                                                    const float* __restrict__ ts_raw, int C, int P, long BN,
+                                                    bf16* __restrict__ xt, bf16* __restrict__ tgt,
+                                                    float* __restrict__ ts_out) {
+  extern __shared__ float tile[];  // [2][C][P+1]
+  const long fr = blockIdx.x;
+  if (fr >= BN) return;
+  const float t = rb(1.f / (1.f + __expf(-rb(ts_raw[fr]))));  // bf16 sigmoid of the bf16 draw
+  if (threadIdx.x == 0 && ts_out) ts_out[fr] = t;
+  const float omt = rb(1.f - t);
+  const long base = fr * (long)C * P;
+  for (int i = threadIdx.x; i < C * P; i += 256) {
+    const float xv = (float)x[base + i], zv = (float)z[base + i];
+    const int c = i / P, pp = i % P;
+    tile[c * (P + 1) + pp] = rb(rb(xv * omt) + rb(zv * t));
+    tile[C * (P + 1) + c * (P + 1) + pp] = rb(zv - xv);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * P; i += 256) {
+    const int pp = i / C, c = i % C;
+    const long o = (fr * P + pp) * (long)C + c;
+    xt[o] = (bf16)tile[c * (P + 1) + pp];
+    tgt[o] = (bf16)tile[C * (P + 1) + c * (P + 1) + pp];
+  }
+}
+
+// token-major [B, N*P, C] -> [B, N, C, P] (unpatchify, gamerft.py:58)
+__global__ __launch_bounds__(256) void unpatchify_k(const bf16* __restrict__ tok, int C, int P, long BN,
+                                                    bf16* __restrict__ out) {
+  extern __shared__ float tile[];
+  const long fr = blockIdx.x;
+  if (fr >= BN) return;
+  for (int i = threadIdx.x; i < C * P; i += 256) {
+    const int pp = i / C, c = i % C;
+    tile[c * (P + 1) + pp] = (float)tok[(fr * P + pp) * (long)C + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * P; i += 256) out[fr * (long)C * P + i] = (bf16)tile[(i / P) * (P + 1) + i % P];
+}
+
+// ------------------------------------------------------------------ MSE loss + gradient
+// partial[block] = sum (pred - tgt)^2 over the block's elements; dpred = bf16(scale*(pred-tgt))
+__global__ __launch_bounds__(256) void mse_k(const bf16* __restrict__ pred, const bf16* __restrict__ tgt, long n8,
+                                             float gscale, bf16* __restrict__ dpred, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float p[8], t[8], g[8];
+    unpack8(((const bf16x8*)pred)[i], p);
+    unpack8(((const bf16x8*)tgt)[i], t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float df = p[e] - t[e];
+      acc += df * df;
+      g[e] = gscale * df;
+    }
+    if (dpred) ((bf16x8*)dpred)[i] = pack8(g);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// ------------------------------------------------------------------ column sums (bias grads)
+// out[n] (+)= sum_r x[r, n]; x bf16 or fp32; grid.y splits the rows, fp32 atomics combine
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R, long N, long ld, long rows_per,
+                                                float* __restrict__ out) {
+  const long col = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (col >= N) return;
+  const long r0 = (long)blockIdx.y * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long r = r0; r < r1; ++r) {
+    if constexpr (sizeof(T) == 2) {
+      float v[8];
+      unpack8(*(const bf16x8*)(x + r * ld + col), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    } else {
+      const f32x4 a = *(const f32x4*)(x + r * ld + col), b = *(const f32x4*)(x + r * ld + col + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[e] += a[e];
+        acc[e + 4] += b[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) atomicAdd(out + col + e, acc[e]);
+}
+
+// ------------------------------------------------------------------ attention-bwd preprocess
+// delta[b, h, t] = sum_d dO[t, h, d] * O[t, h, d]   (fp32; D = 64/128 -> 8/16 lanes per row)
+template <int D>
+__global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                                    long ld, long L, int H, long nrows, float* __restrict__ delta) {
+  constexpr int CPR = D / 8;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rowid = gid / CPR;  // (b, t, h) in token-major order
+  const int j = gid % CPR;
+  if (rowid >= nrows) return;
+  const long bt = rowid / H;
+  const int h = rowid % H;
+  float a[8], b[8];
+  unpack8(*(const bf16x8*)(o + bt * ld + (long)h * D + j * 8), a);
+  unpack8(*(const bf16x8*)(dout + bt * ld + (long)h * D + j * 8), b);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += a[e] * b[e];
+#pragma unroll
+  for (int off = 1; off < CPR; off <<= 1) s += __shfl_xor(s, off, 64);
+  if (j == 0) {
+    const long bb = bt / L, t = bt % L;
+    delta[(bb * H + h) * L + t] = s;
+  }
+}
+
+}  // namespace
+
+// ======================================================================== C ABI
+extern "C" int owlk_adaln_fwd(const void* x, long ldx, const void* scale, const void* shift, long ldm, long tpf,
+                              long T, int d, void* y, long ldy, float* rstd, void* yact, void* stream) {
+  OWLK_REQUIRE(d % 8 == 0 && d <= 64 * 8 * MAXCPL && tpf > 0 && T % tpf == 0, "adaln_fwd: bad d=%d tpf=%ld T=%ld", d,
+               tpf, T);
+  OWLK_CPL_DISPATCH(d, adaln_fwd_k, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
+                     ldx, (const bf16*)scale, (const bf16*)shift, ldm, tpf, T, d, (bf16*)y, ldy, rstd, (bf16*)yact);
+  return owlk::check_launch("adaln_fwd");
+}
+
+extern "C" int owlk_adaln_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd,
+                              const void* scale, long ldm, long tpf, long T, int d, const void* dres, long ldres,
+                              void* dx, long lddx, float* dscale, float* dshift, long ldg, const void* ypre,
+                              void* stream) {
+  OWLK_REQUIRE(d % 8 == 0 && d <= 64 * 8 * MAXCPL && tpf > 0 && T % tpf == 0, "adaln_bwd: bad d=%d tpf=%ld T=%ld", d,
+               tpf, T);
+  OWLK_CPL_DISPATCH(d, adaln_bwd_k, dim3((unsigned)(T / tpf)), dim3(256), 8 * d * sizeof(float), (hipStream_t)stream,
+                     (const bf16*)dy, lddy, (const bf16*)x, ldx, rstd, (const bf16*)scale, ldm, tpf, d,
+                     (const bf16*)dres, ldres, (bf16*)dx, lddx, dscale, dshift, ldg, (const bf16*)ypre);
+  return owlk::check_launch("adaln_bwd");
+}
+
+extern "C" int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const void* g, long ldg, long tpf,
+                             long T, int d, void* dy, long lddy, float* dg, float* dbias_frames, long ldr,
+                             void* stream) {
+  OWLK_REQUIRE(d % 8 == 0 && d <= 64 * 8 * MAXCPL && tpf > 0 && T % tpf == 0, "gate_bwd: bad d=%d tpf=%ld T=%ld", d,
+               tpf, T);
+  OWLK_CPL_DISPATCH(d, gate_bwd_k, dim3((unsigned)(T / tpf)), dim3(256), 8 * d * sizeof(float), (hipStream_t)stream,
+                     (const bf16*)dout, ldo, (const bf16*)y, ldy, (const bf16*)g, ldg, tpf, d, (bf16*)dy, lddy, dg,
+                     dbias_frames, ldr);
+  return owlk::check_launch("gate_bwd");
+}
+
+extern "C" int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const float* cosb,
+                                const float* sinb, long ld_tab, long tab_off, long tpos_div, void* out, long ldo,
+                                float* rstd, void* stream) {
+  OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_fwd: head_dim %d unsupported", D);
+  const long threads = T * 2 * H * (D / 8);
+  dim3 g((unsigned)((threads + 255) / 256));
+  if (D == 64)
+    hipLaunchKernelGGL(qk_rope_fwd_k<64>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, H, cosb,
+                       sinb, ld_tab, tab_off, tpos_div, (bf16*)out, ldo, rstd);
+  else
+    hipLaunchKernelGGL(qk_rope_fwd_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, H, cosb,
+                       sinb, ld_tab, tab_off, tpos_div, (bf16*)out, ldo, rstd);
+  return owlk::check_launch("qk_rope_fwd");
+}
+
+extern "C" int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
+                                const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
+                                const float* rstd, void* dqkv, long ldg, void* stream) {
+  OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_bwd: head_dim %d unsupported", D);
+  const long threads = T * 2 * H * (D / 8);
+  dim3 g((unsigned)((threads + 255) / 256));
+  if (D == 64)
+    hipLaunchKernelGGL(qk_rope_bwd_k<64>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)dqk, ldd,
+                       (const bf16*)qkv, ldq, T, H, cosb, sinb, ld_tab, tab_off, tpos_div, rstd, (bf16*)dqkv, ldg);
+  else
+    hipLaunchKernelGGL(qk_rope_bwd_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)dqk, ldd,
+                       (const bf16*)qkv, ldq, T, H, cosb, sinb, ld_tab, tab_off, tpos_div, rstd, (bf16*)dqkv, ldg);
+  return owlk::check_launch("qk_rope_bwd");
+}
+
+extern "C" int owlk_flow_noise(const void* x, const void* z, const float* ts_raw, int C, int P, long BN, void* xt,
+                               void* tgt, float* ts_out, void* stream) {
+  OWLK_REQUIRE(C * P <= 16384 && C > 0 && P > 0, "flow_noise: C*P too large");
+  hipLaunchKernelGGL(flow_noise_k, dim3((unsigned)BN), dim3(256), 2 * C * (P + 1) * sizeof(float),
+                     (hipStream_t)stream, (const bf16*)x, (const bf16*)z, ts_raw, C, P, BN, (bf16*)xt, (bf16*)tgt,
+                     ts_out);
+  return owlk::check_launch("flow_noise");
+}
+
+extern "C" int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out, void* stream) {
+  OWLK_REQUIRE(C * P <= 16384, "unpatchify: C*P too large");
+  hipLaunchKernelGGL(unpatchify_k, dim3((unsigned)BN), dim3(256), C * (P + 1) * sizeof(float), (hipStream_t)stream,
+                     (const bf16*)tok, C, P, BN, (bf16*)out);
+  return owlk::check_launch("unpatchify");
+}
+
+extern "C" int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,
+                        int nblocks, void* stream) {
+  OWLK_REQUIRE(n % 8 == 0 && nblocks > 0, "mse: n=%ld must be a multiple of 8", n);
+  hipLaunchKernelGGL(mse_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const bf16*)pred, (const bf16*)tgt,
+                     n / 8, gscale, (bf16*)dpred, partial);
+  return owlk::check_launch("mse");
+}
+
+extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream) {
+  OWLK_REQUIRE(N % 8 == 0 && ld % 8 == 0, "colsum: N, ld must be multiples of 8");
+  const long cols_blocks = (N / 8 + 255) / 256;
+  long splits = 1024 / cols_blocks;
+  if (splits < 1) splits = 1;
+  if (splits > R) splits = R;
+  const long rows_per = (R + splits - 1) / splits;
+  dim3 g((unsigned)cols_blocks, (unsigned)((R + rows_per - 1) / rows_per));
+  if (x_f32)
+    hipLaunchKernelGGL(colsum_k<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)x, R, N, ld, rows_per,
+                       out);
+  else
+    hipLaunchKernelGGL(colsum_k<bf16>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, R, N, ld, rows_per,
+                       out);
+  return owlk::check_launch("colsum");
+}
+
+extern "C" int owlk_attn_delta(const void* o, const void* dout, long ld, long B, long L, int H, int D, float* delta,
+                               void* stream) {
+  OWLK_REQUIRE(D == 64 || D == 128, "attn_delta: head_dim %d unsupported", D);
+  const long nrows = B * L * H;
+  const long threads = nrows * (D / 8);
+  dim3 g((unsigned)((threads + 255) / 256));
+  if (D == 64)
+    hipLaunchKernelGGL(attn_delta_k<64>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)o, (const bf16*)dout, ld,
+                       L, H, nrows, delta);
+  else
+    hipLaunchKernelGGL(attn_delta_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)o, (const bf16*)dout,
+                       ld, L, H, nrows, delta);
+  return owlk::check_launch("attn_delta");
+}

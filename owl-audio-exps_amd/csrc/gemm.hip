@@ -1,0 +1,350 @@
+// bf16 MFMA GEMM with fused epilogues for the owl_wms DiT training step (gfx950).
+//
+//   C[m, n] = epi( sum_k A(m, k) * B(n, k) )
+//
+//   A(m, k) = A[m*lda + k]   (a_trans = 0, k-contiguous)   or  A[k*lda + m]  (a_trans = 1)
+//   B(n, k) = B[n*ldb + k]   (b_trans = 0, k-contiguous)   or  B[k*ldb + n]  (b_trans = 1)
+//
+// Replaces every cuBLAS nn.Linear GEMM of the reference hot path (SURVEY.md §2.2 row
+// "cuBLAS nn.Linear"): forward y = x W^T (+b) uses (0,0); dX = dY W uses (0,1); dW = dY^T X
+// uses (1,1).  Tiles: BM x BN x 64, 4 waves (2x2), v_mfma_f32_16x16x32_bf16, operands staged
+// global -> VGPR -> LDS (double buffered, one barrier per K-step).  k-contiguous tiles are
+// XOR-swizzled for conflict-free ds_read_b128; m/n-contiguous tiles are read with the
+// ds_read_b64_tr_b16 hardware transpose through a 32-B block swizzle.  The epilogue goes
+// through LDS so every global access is a 16-B row chunk.
+#include "common.hpp"
+
+namespace {
+
+enum Epi : int {
+  EPI_STORE = 0,       // C = alpha*acc (+ bf16(bias)) (+ beta*C_old)
+  EPI_SILU = 1,        // aux = bf16(acc + bias); C = bf16(silu(aux))            (MLP fc1)
+  EPI_GATE_RESID = 2,  // aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m/tpf]*y))
+  EPI_DSILU = 3,       // C = bf16(bf16(acc) * silu'(aux))                        (MLP fc1 bwd)
+  EPI_AXPBY = 4,       // C = bf16(bf16(alpha*bf16(acc)) + bf16(beta*aux))        (Newton-Schulz)
+};
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+struct GemmP {
+  long M, N, K;
+  const bf16* A; long lda, sA;
+  const bf16* B; long ldb, sB;
+  void* C; long ldc, sC;
+  float alpha, beta;
+  const float* bias;
+  bf16* aux; long ldaux, sAux;
+  const bf16* gate; long ldgate, sGate, tpf;
+  const bf16* resid; long ldres, sRes;
+  int tiles_m, tiles_n;
+};
+
+// 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
+// touches land on distinct bank slots (256-B rows for ROWS >= 128, 128-B rows for ROWS == 64)
+template <int ROWS>
+DEV int swz_t(int k) {
+  if (ROWS >= 128) return (k & 3) | (((k >> 3) & 1) << 2);
+  return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);
+}
+
+// ---- staging: global -> registers for one operand tile (ROWS x 64 along k) ---------------
+template <int ROWS, bool TRANS>
+struct Stager {
+  static constexpr int CHUNKS = ROWS * BK / 8;  // 16-byte chunks in the tile
+  static constexpr int PER = CHUNKS / NT;
+  bf16x8 r[PER];
+
+  DEV void load(const bf16* base, long ld, long r0, long k0, long R, long K) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT;
+      long row, col;
+      bool ok;
+      if (!TRANS) {  // [ROWS][64]: 8 chunks per row
+        row = r0 + (c >> 3);
+        col = k0 + (c & 7) * 8;
+        ok = row < R && col < K;
+        r[i] = ok ? *(const bf16x8*)(base + row * ld + col) : bf16x8{};
+      } else {  // [64][ROWS]: ROWS/8 chunks per k-row
+        constexpr int CPR = ROWS / 8;
+        row = k0 + c / CPR;
+        col = r0 + (c % CPR) * 8;
+        ok = row < K && col < R;
+        r[i] = ok ? *(const bf16x8*)(base + row * ld + col) : bf16x8{};
+      }
+    }
+  }
+
+  DEV void store(char* lds) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT;
+      int off;
+      if (!TRANS) {
+        const int row = c >> 3, kc = c & 7;
+        off = row * 128 + ((kc ^ ((row >> 1) & 7)) << 4);
+      } else {
+        constexpr int CPR = ROWS / 8;
+        const int k = c / CPR, mc = c % CPR;
+        off = k * (ROWS * 2) + (((mc >> 1) ^ swz_t<ROWS>(k)) << 5) + ((mc & 1) << 4);
+      }
+      *(bf16x8*)(lds + off) = r[i];
+    }
+  }
+};
+
+// fragment (8 bf16 along k) for rows [row0, row0+16) of an LDS operand tile, k-substep kk
+template <int ROWS, bool TRANS>
+DEV bf16x8 read_frag(const char* lds, int row0, int kk, int lane) {
+  if (!TRANS) {
+    const int r = row0 + (lane & 15);
+    const int kc = 4 * kk + (lane >> 4);
+    return *(const bf16x8*)(lds + r * 128 + ((kc ^ ((r >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int blk = row0 >> 4;
+    const int k0 = 32 * kk + 8 * g + q;
+    const int k1 = k0 + 4;
+    s16x4 lo = ds_read_tr16(lds + k0 * (ROWS * 2) + ((blk ^ swz_t<ROWS>(k0)) << 5) + pp * 8);
+    s16x4 hi = ds_read_tr16(lds + k1 * (ROWS * 2) + ((blk ^ swz_t<ROWS>(k1)) << 5) + pp * 8);
+    return join_tr(lo, hi);
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT, int EPI, bool OF32>
+__global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
+  constexpr int WTM = BM / 2, WTN = BN / 2;  // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = 2 * (A_BYTES + B_BYTES);
+  constexpr int EPI_LD = BN + 4;
+  constexpr int EPI_BYTES = BM * EPI_LD * 4;
+  constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap of the linear tile id (MI355X_MICROARCH: blocks b, b+8 share an XCD)
+  const int nwg = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+  const long z = blockIdx.z;
+  const bf16* A = p.A + z * p.sA;
+  const bf16* B = p.B + z * p.sB;
+
+  Stager<BM, AT> sa;
+  Stager<BN, BT> sb;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)((p.K + BK - 1) / BK);
+  sa.load(A, p.lda, m0, 0, p.M, p.K);
+  sb.load(B, p.ldb, n0, 0, p.N, p.K);
+  sa.store(smem);
+  sb.store(smem + A_BYTES);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(A, p.lda, m0, (long)(kt + 1) * BK, p.M, p.K);
+      sb.load(B, p.ldb, n0, (long)(kt + 1) * BK, p.N, p.K);
+    }
+    const char* la = smem + cur * (A_BYTES + B_BYTES);
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = read_frag<BM, AT>(la, wm * WTM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, BT>(lb, wn * WTN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* nb = smem + (cur ^ 1) * (A_BYTES + B_BYTES);
+      sa.store(nb);
+      sb.store(nb + A_BYTES);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: accumulators -> LDS fp32 tile -> 16-B row chunks -------------------------
+  float* ct = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + 16 * j + (lane & 15);
+      const int row = wm * WTM + 16 * i + (lane >> 4) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ct[(row + r) * EPI_LD + col] = acc[i][j][r];
+    }
+  __syncthreads();
+
+  constexpr int CH = BM * BN / 8;
+  for (int c = threadIdx.x; c < CH; c += NT) {
+    const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
+    const long gm = m0 + row, gn = n0 + col;
+    if (gm >= p.M || gn >= p.N) continue;  // N % 8 == 0 is required by the host
+    float v[8];
+    {
+      const f32x4 lo = *(const f32x4*)(ct + row * EPI_LD + col);
+      const f32x4 hi = *(const f32x4*)(ct + row * EPI_LD + col + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e];
+        v[e + 4] = hi[e];
+      }
+    }
+    float bb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bb[e] = p.bias ? rb(p.bias[gn + e]) : 0.f;
+
+    if (EPI == EPI_STORE) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
+      if (OF32) {
+        float* C = (float*)p.C + z * p.sC + gm * p.ldc + gn;
+        if (p.beta != 0.f) {
+          const f32x4 o0 = *(const f32x4*)C, o1 = *(const f32x4*)(C + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] += p.beta * o0[e];
+            v[e + 4] += p.beta * o1[e];
+          }
+        }
+        *(f32x4*)C = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        bf16* C = (bf16*)p.C + z * p.sC + gm * p.ldc + gn;
+        if (p.beta != 0.f) {
+          float o[8];
+          unpack8(*(const bf16x8*)C, o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += p.beta * o[e];
+        }
+        *(bf16x8*)C = pack8(v);
+      }
+    } else if (EPI == EPI_SILU) {
+      float y[8], s[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        y[e] = rb(v[e] + bb[e]);
+        s[e] = silu_f(y[e]);
+      }
+      *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
+      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(s);
+    } else if (EPI == EPI_GATE_RESID) {
+      float y[8], g[8], r[8], o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = rb(v[e] + bb[e]);
+      unpack8(*(const bf16x8*)(p.gate + z * p.sGate + (gm / p.tpf) * p.ldgate + gn), g);
+      unpack8(*(const bf16x8*)(p.resid + z * p.sRes + gm * p.ldres + gn), r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = r[e] + rb(g[e] * y[e]);
+      if (p.aux) *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
+      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    } else if (EPI == EPI_DSILU) {
+      float x[8], o[8];
+      unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sg = 1.f / (1.f + __expf(-x[e]));
+        o[e] = rb(v[e]) * sg * (1.f + x[e] * (1.f - sg));
+      }
+      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    } else if (EPI == EPI_AXPBY) {
+      float x[8], o[8];
+      unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * x[e]));
+      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    }
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT, int EPI, bool OF32>
+int launch(GemmP& p, long batch, hipStream_t s) {
+  p.tiles_m = (int)((p.M + BM - 1) / BM);
+  p.tiles_n = (int)((p.N + BN - 1) / BN);
+  dim3 grid(p.tiles_m * p.tiles_n, 1, (unsigned)batch);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AT, BT, EPI, OF32>), grid, dim3(NT), 0, s, p);
+  return owlk::check_launch("gemm");
+}
+
+template <int BM, int BN, int EPI, bool OF32>
+int dispatch_t(GemmP& p, int at, int bt, long batch, hipStream_t s) {
+  if (!at && !bt) return launch<BM, BN, false, false, EPI, OF32>(p, batch, s);
+  if (!at && bt) return launch<BM, BN, false, true, EPI, OF32>(p, batch, s);
+  if (at && bt) return launch<BM, BN, true, true, EPI, OF32>(p, batch, s);
+  return launch<BM, BN, true, false, EPI, OF32>(p, batch, s);
+}
+
+template <int BM, int BN>
+int dispatch_e(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE:
+      return cf32 ? dispatch_t<BM, BN, EPI_STORE, true>(p, at, bt, batch, s)
+                  : dispatch_t<BM, BN, EPI_STORE, false>(p, at, bt, batch, s);
+    case EPI_SILU: return dispatch_t<BM, BN, EPI_SILU, false>(p, at, bt, batch, s);
+    case EPI_GATE_RESID: return dispatch_t<BM, BN, EPI_GATE_RESID, false>(p, at, bt, batch, s);
+    case EPI_DSILU: return dispatch_t<BM, BN, EPI_DSILU, false>(p, at, bt, batch, s);
+    case EPI_AXPBY: return dispatch_t<BM, BN, EPI_AXPBY, false>(p, at, bt, batch, s);
+  }
+  owlk::set_error("gemm: unknown epilogue %d", epi);
+  return 1;
+}
+
+}  // namespace
+
+extern "C" int owlk_gemm(long M, long N, long K, long batch,
+                         const void* A, long lda, long sA, int a_trans,
+                         const void* B, long ldb, long sB, int b_trans,
+                         void* C, long ldc, long sC, int c_f32,
+                         int epi, float alpha, float beta, const float* bias,
+                         void* aux, long ldaux, long sAux,
+                         const void* gate, long ldgate, long sGate, long tpf,
+                         const void* resid, long ldres, long sRes,
+                         void* stream) {
+  OWLK_REQUIRE(M > 0 && N > 0 && K > 0 && batch > 0, "gemm: bad sizes M=%ld N=%ld K=%ld b=%ld", M, N, K, batch);
+  OWLK_REQUIRE(N % 8 == 0, "gemm: N=%ld must be a multiple of 8", N);
+  OWLK_REQUIRE(a_trans ? (M % 8 == 0) : (K % 8 == 0), "gemm: A contiguous dim must be a multiple of 8");
+  OWLK_REQUIRE(b_trans ? (N % 8 == 0) : (K % 8 == 0), "gemm: B contiguous dim must be a multiple of 8");
+  OWLK_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "gemm: leading dims must be multiples of 8");
+  OWLK_REQUIRE(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "gemm: operands must be 16-byte aligned");
+  OWLK_REQUIRE(!c_f32 || epi == EPI_STORE, "gemm: fp32 output only with EPI_STORE");
+  OWLK_REQUIRE(epi != EPI_GATE_RESID || (gate && resid && tpf > 0), "gemm: gate epilogue needs gate/resid/tpf");
+  OWLK_REQUIRE(!(epi == EPI_SILU || epi == EPI_DSILU || epi == EPI_AXPBY) || aux, "gemm: epilogue needs aux");
+  GemmP p{};
+  p.M = M; p.N = N; p.K = K;
+  p.A = (const bf16*)A; p.lda = lda; p.sA = sA;
+  p.B = (const bf16*)B; p.ldb = ldb; p.sB = sB;
+  p.C = C; p.ldc = ldc; p.sC = sC;
+  p.alpha = alpha; p.beta = beta; p.bias = bias;
+  p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux;
+  p.gate = (const bf16*)gate; p.ldgate = ldgate; p.sGate = sGate; p.tpf = tpf > 0 ? tpf : 1;
+  p.resid = (const bf16*)resid; p.ldres = ldres; p.sRes = sRes;
+  hipStream_t s = (hipStream_t)stream;
+  // small outputs (per-frame modulation, Newton-Schulz) use 64x64 tiles to fill the chip
+  const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
+  if (tiles128 < 512) return dispatch_e<64, 64>(p, a_trans, b_trans, epi, c_f32, batch, s);
+  return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
+}

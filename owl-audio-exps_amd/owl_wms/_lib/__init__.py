@@ -1,0 +1,72 @@
+"""ctypes binding of libowlk.so (the C ABI declared in include/owlk.h).
+
+The library is built in-tree by ``owl-audio-exps_amd/csrc/Makefile`` (``__graft_entry__.build()``).
+It is loaded after ``torch`` so it binds to the HIP runtime torch already loaded (same SONAME).
+There is no fallback: if the library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libowlk.so")
+
+L, I, F, P = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
+
+_SIGS = {
+    "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P],
+    "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
+    "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
+    "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],
+    "owlk_qk_rope_fwd": [P, L, L, I, I, P, P, L, L, L, P, L, P, P],
+    "owlk_qk_rope_bwd": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P],
+    "owlk_attn_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, L, I, F, L, I, I, L, P, P, P, P, L, P],
+    "owlk_attn_delta": [P, P, L, L, L, I, I, P, P],
+    "owlk_attn_bwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I, I,
+                      P, P, P, P, L, P],
+    "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
+    "owlk_unpatchify": [P, I, I, L, P, P],
+    "owlk_mse": [P, P, L, F, P, P, I, P],
+    "owlk_colsum": [P, I, L, L, L, P, P],
+    "owlk_ns_normalize": [P, I, L, L, L, I, P, P, P],
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libowlk.so not built at {LIB_PATH}: run `make -C owl-audio-exps_amd/csrc` "
+                               "(or __graft_entry__.build()); there is no non-HIP fallback")
+        h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        h.owlk_last_error.restype = ctypes.c_char_p
+        h.owlk_last_error.argtypes = []
+        h.owlk_version.restype = ctypes.c_int
+        h.owlk_device_ok.restype = ctypes.c_int
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return ["owlk_last_error", "owlk_version", "owlk_device_ok"] + list(_SIGS)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed ({rc}): {lib().owlk_last_error().decode()}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -1,0 +1,42 @@
+"""Data (reference: owl_wms/data/).  The real S3/NpyTable loaders are out of scope;
+``synthetic`` yields batches of the configured latent shape for benchmarking and
+plumbing runs, with the reference's batch tuple layout."""
+import torch
+
+
+def synthetic_video_batch(cfg, batch_size, seed=1234, n_docs=1, device="cpu"):
+    """(vid [b,n,c,h,w] bf16, mouse [b,n,2] bf16, btn [b,n,n_buttons] bf16, doc_id [b,n] int64)."""
+    g = torch.Generator().manual_seed(seed)
+    n, c, s = cfg.n_frames, cfg.channels, cfg.sample_size
+    vid = torch.randn(batch_size, n, c, s, s, generator=g).to(torch.bfloat16)
+    mouse = torch.randn(batch_size, n, 2, generator=g).to(torch.bfloat16)
+    btn = (torch.rand(batch_size, n, cfg.n_buttons, generator=g) < 0.5).to(torch.bfloat16)
+    doc = (torch.arange(n) * n_docs // n).expand(batch_size, n).contiguous()
+    return [t.to(device) for t in (vid, mouse, btn, doc)]
+
+
+def synthetic_audio_batch(cfg, batch_size, seed=1234, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(batch_size, cfg.sample_size, cfg.channels, generator=g).to(device)
+
+
+class SyntheticLoader:
+    def __init__(self, make, n_batches):
+        self.make, self.n = make, n_batches
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        for i in range(self.n):
+            yield self.make(i)
+
+
+def get_loader(data_id, batch_size, model_cfg=None, n_batches=10 ** 9, **kwargs):
+    if data_id in ("synthetic", "sequence_packing", "cod", "synthetic_video"):
+        return SyntheticLoader(lambda i: synthetic_video_batch(model_cfg, batch_size, seed=1234 + i,
+                                                               n_docs=kwargs.get("n_docs", 1)), n_batches)
+    if data_id in ("synthetic_audio", "local_waveform"):
+        return SyntheticLoader(lambda i: synthetic_audio_batch(model_cfg, batch_size, seed=1234 + i), n_batches)
+    raise NotImplementedError(f"data_id {data_id!r}: only synthetic latents are supported on this build "
+                              "(real S3/NpyTable loaders are out of scope, SURVEY.md §2.1)")

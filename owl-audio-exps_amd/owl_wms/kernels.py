@@ -1,0 +1,257 @@
+"""Typed Python wrappers over libowlk (include/owlk.h).  Device tensors in, device tensors out.
+
+Every function checks shapes/strides on the host before the launch (a kernel never sees an
+operand its grid does not cover) and enqueues on torch's current HIP stream.
+"""
+import torch
+
+from ._lib import call, ptr, stream
+
+BF16, F32 = torch.bfloat16, torch.float32
+
+EPI_STORE, EPI_SILU, EPI_GATE_RESID, EPI_DSILU, EPI_AXPBY = 0, 1, 2, 3, 4
+
+
+def _rowmajor(t, name):
+    assert t.dim() == 2 and t.stride(1) == 1, f"{name} must be a row-major 2-D view (got {t.shape}/{t.stride()})"
+    assert t.dtype == BF16, f"{name} must be bf16"
+    return t
+
+
+def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI_STORE, alpha=1.0, beta=0.0,
+         bias=None, aux=None, gate=None, tpf=1, resid=None):
+    """C[m, n] = epi(sum_k A(m, k) B(n, k)) for 2-D views.
+
+    A: [M, K] (a_trans False) or [K, M] (a_trans True); B: [N, K] or [K, N] (b_trans True).
+    """
+    _rowmajor(A, "A")
+    _rowmajor(B, "B")
+    M, K = (A.shape[1], A.shape[0]) if a_trans else (A.shape[0], A.shape[1])
+    N, Kb = (B.shape[1], B.shape[0]) if b_trans else (B.shape[0], B.shape[1])
+    assert K == Kb, f"gemm: K mismatch {K} vs {Kb}"
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=F32 if out_f32 else BF16)
+    assert out.shape == (M, N) and out.stride(1) == 1
+    assert out.dtype == (F32 if out_f32 else BF16)
+    if bias is not None:
+        assert bias.dtype == F32 and bias.numel() == N and bias.is_contiguous()
+    for t, nm in ((aux, "aux"), (resid, "resid")):
+        if t is not None:
+            assert t.shape == (M, N) and t.stride(1) == 1 and t.dtype == BF16, nm
+    if gate is not None:
+        assert gate.dim() == 2 and gate.shape[1] == N and gate.stride(1) == 1 and gate.shape[0] * tpf >= M
+    call("owlk_gemm", M, N, K, 1,
+         ptr(A), A.stride(0), 0, int(a_trans),
+         ptr(B), B.stride(0), 0, int(b_trans),
+         ptr(out), out.stride(0), 0, int(out_f32),
+         epi, float(alpha), float(beta), ptr(bias),
+         ptr(aux), aux.stride(0) if aux is not None else 0, 0,
+         ptr(gate), gate.stride(0) if gate is not None else 0, 0, int(tpf),
+         ptr(resid), resid.stride(0) if resid is not None else 0, 0,
+         stream())
+    return out
+
+
+def bgemm(A, B, out, *, a_trans=False, b_trans=False, epi=EPI_STORE, alpha=1.0, beta=0.0, aux=None):
+    """Batched GEMM over dim 0 of 3-D row-major tensors (Newton-Schulz)."""
+    bt = A.shape[0]
+    M, K = (A.shape[2], A.shape[1]) if a_trans else (A.shape[1], A.shape[2])
+    N, Kb = (B.shape[2], B.shape[1]) if b_trans else (B.shape[1], B.shape[2])
+    assert K == Kb and out.shape == (bt, M, N)
+    for t in (A, B, out) + ((aux,) if aux is not None else ()):
+        assert t.dtype == BF16 and t.is_contiguous()
+    call("owlk_gemm", M, N, K, bt,
+         ptr(A), A.stride(1), A.stride(0), int(a_trans),
+         ptr(B), B.stride(1), B.stride(0), int(b_trans),
+         ptr(out), out.stride(1), out.stride(0), 0,
+         epi, float(alpha), float(beta), None,
+         ptr(aux), aux.stride(1) if aux is not None else 0, aux.stride(0) if aux is not None else 0,
+         None, 0, 0, 1, None, 0, 0, stream())
+    return out
+
+
+def adaln_fwd(x, scale, shift, tpf, act=False):
+    """x [T, d] bf16; scale/shift [F, d] views (row stride ldm) -> y [T, d], rstd [T] (, silu(y))."""
+    T, d = x.shape
+    assert x.stride(1) == 1 and scale.stride(1) == 1 and shift.stride(1) == 1
+    assert scale.stride(0) == shift.stride(0) and scale.shape[0] * tpf == T
+    y = torch.empty(T, d, device=x.device, dtype=BF16)
+    ya = torch.empty_like(y) if act else None
+    rstd = torch.empty(T, device=x.device, dtype=F32)
+    call("owlk_adaln_fwd", ptr(x), x.stride(0), ptr(scale), ptr(shift), scale.stride(0), tpf, T, d, ptr(y), d,
+         ptr(rstd), ptr(ya), stream())
+    return (y, rstd, ya) if act else (y, rstd)
+
+
+def adaln_bwd(dy, x, rstd, scale, tpf, dres=None, ypre=None):
+    """-> dx [T, d] bf16 (+ dres), dmod [F, 2d] fp32 (= [dscale | dshift])."""
+    T, d = x.shape
+    F_ = T // tpf
+    dx = torch.empty(T, d, device=x.device, dtype=BF16)
+    dmod = torch.empty(F_, 2 * d, device=x.device, dtype=F32)
+    call("owlk_adaln_bwd", ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(rstd), ptr(scale), scale.stride(0), tpf,
+         T, d, ptr(dres), dres.stride(0) if dres is not None else 0, ptr(dx), d, ptr(dmod), ptr(dmod[:, d:]), 2 * d,
+         ptr(ypre), stream())
+    return dx, dmod
+
+
+def gate_bwd(dout, y, g, tpf, want_bias=True):
+    """-> dy [T, d] bf16, dg [F, d] fp32, per-frame bias partials [F, d] fp32 (or None)."""
+    T, d = y.shape
+    F_ = T // tpf
+    dy = torch.empty(T, d, device=y.device, dtype=BF16)
+    dg = torch.empty(F_, d, device=y.device, dtype=F32)
+    dbf = torch.empty(F_, d, device=y.device, dtype=F32) if want_bias else None
+    call("owlk_gate_bwd", ptr(dout), dout.stride(0), ptr(y), y.stride(0), ptr(g), g.stride(0), tpf, T, d, ptr(dy), d,
+         ptr(dg), ptr(dbf), d, stream())
+    return dy, dg, dbf
+
+
+def qk_rope_fwd(qkv, H, D, cos, sin, tab_off=0, tpos_div=0):
+    """qkv [T, 3 H D] -> out [T, 2 H D] (rotated q | k), rstd [T, 2H]."""
+    T = qkv.shape[0]
+    out = torch.empty(T, 2 * H * D, device=qkv.device, dtype=BF16)
+    rstd = torch.empty(T, 2 * H, device=qkv.device, dtype=F32)
+    call("owlk_qk_rope_fwd", ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin), cos.stride(0), tab_off, tpos_div,
+         ptr(out), out.stride(0), ptr(rstd), stream())
+    return out, rstd
+
+
+def qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, dqkv, tab_off=0, tpos_div=0):
+    T = qkv.shape[0]
+    call("owlk_qk_rope_bwd", ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin),
+         cos.stride(0), tab_off, tpos_div, ptr(rstd), ptr(dqkv), dqkv.stride(0), stream())
+
+
+class FrameMask:
+    """Host-side description of the reference frame mask (attn.py:24-62) for the kernels."""
+
+    def __init__(self, tpf, window=None, causal=True, q_offset=0, arrays=None):
+        self.tpf, self.window, self.causal, self.q_offset = int(tpf), window, bool(causal), int(q_offset)
+        self.arrays = arrays  # dict kv_lo, q_hi, run_start, doc: int32 [B, n_frames] or None
+
+    def args(self):
+        a = self.arrays
+        w = 0 if self.window is None else int(self.window)
+        if a is None:
+            return (self.tpf, w, int(self.causal), None, None, None, None, 0)
+        return (self.tpf, w, int(self.causal), ptr(a["kv_lo"]), ptr(a["q_hi"]), ptr(a["run_start"]), ptr(a["doc"]),
+                a["doc"].stride(0))
+
+
+def frame_arrays(doc_id, n_frames, window, causal=True):
+    """Per-frame helper arrays for a [B, n_frames] doc_id (any integer ids, runs or not)."""
+    B = doc_id.shape[0]
+    dev = doc_id.device
+    doc = doc_id[:, :n_frames].to(torch.int64)
+    idx = torch.arange(n_frames, device=dev).expand(B, n_frames)
+    boundary = torch.ones_like(doc, dtype=torch.bool)
+    boundary[:, 1:] = doc[:, 1:] != doc[:, :-1]
+    run_start = torch.cummax(torch.where(boundary, idx, torch.zeros_like(idx)), dim=1).values
+    # first / last occurrence of each frame's doc id (documents need not be contiguous)
+    first = torch.empty_like(doc)
+    last = torch.empty_like(doc)
+    for b in range(B):
+        _, inv = torch.unique(doc[b], return_inverse=True)
+        k = int(inv.max().item()) + 1
+        fo = torch.full((k,), n_frames, device=dev, dtype=torch.int64).scatter_reduce(0, inv, idx[b], "amin")
+        lo = torch.full((k,), -1, device=dev, dtype=torch.int64).scatter_reduce(0, inv, idx[b], "amax")
+        first[b], last[b] = fo[inv], lo[inv]
+    if window is None:
+        kv_lo = first
+        q_hi = last
+    else:
+        kv_lo = torch.maximum(first, idx - window + 1)
+        q_hi = torch.minimum(last, idx + window - 1)
+    if not causal:
+        pass  # kernels widen the kv range symmetrically from the window themselves
+    i32 = torch.int32
+    return {"kv_lo": kv_lo.to(i32).contiguous(), "q_hi": q_hi.to(i32).contiguous(),
+            "run_start": run_start.to(i32).contiguous(), "doc": doc.to(i32).contiguous()}
+
+
+def _v3(t, name):
+    assert t.dim() == 3 and t.stride(2) == 1 and t.dtype == BF16, f"{name}: need a [B, L, cols] bf16 view"
+    return t
+
+
+def attn_fwd(q, k, v, H, D, mask, scale=None, o=None):
+    """Frame-masked flash attention.  q [B, Lq, >=H*D], k/v [B, Lkv, >=H*D] token-major views
+    (head h at columns h*D); returns o [B, Lq, H*D] bf16 and lse [B, H, Lq] fp32."""
+    _v3(q, "q"), _v3(k, "k"), _v3(v, "v")
+    B, Lq, Lkv = q.shape[0], q.shape[1], k.shape[1]
+    assert k.shape[0] == B and v.shape[:2] == k.shape[:2]
+    scale = D ** -0.5 if scale is None else scale
+    if o is None:
+        o = torch.empty(B, Lq, H * D, device=q.device, dtype=BF16)
+    _v3(o, "o")
+    lse = torch.empty(B, H, Lq, device=q.device, dtype=F32)
+    call("owlk_attn_fwd", ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
+         ptr(v), v.stride(1), v.stride(0), ptr(o), o.stride(1), o.stride(0), ptr(lse), B, H, Lq, Lkv, D,
+         float(scale), mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), mask.q_offset,
+         *mask.args()[3:], stream())
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
+    """Backward of attn_fwd (training shapes: Lq == Lkv, q_offset 0); all tensors [B, L, cols]."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
+        _v3(t, n)
+    B, L = q.shape[:2]
+    scale = D ** -0.5 if scale is None else scale
+    delta = torch.empty(B, H, L, device=q.device, dtype=F32)
+    assert o.is_contiguous() and do.is_contiguous() and o.shape == do.shape
+    call("owlk_attn_delta", ptr(o), ptr(do), o.stride(1), B, L, H, D, ptr(delta), stream())
+    call("owlk_attn_bwd", ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
+         ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
+         ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),
+         ptr(dv), dv.stride(1), dv.stride(0), B, H, L, L, D, float(scale),
+         mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), *mask.args()[3:], stream())
+
+
+def flow_noise(x, z, ts_raw):
+    """x, z [B, N, C, h, w] bf16; ts_raw [B, N] -> xt_tok, tgt_tok [B*N*h*w, C] bf16, ts [B, N] bf16."""
+    B, N, C, h, w = x.shape
+    P = h * w
+    xt = torch.empty(B * N * P, C, device=x.device, dtype=BF16)
+    tgt = torch.empty_like(xt)
+    ts = torch.empty(B, N, device=x.device, dtype=F32)
+    call("owlk_flow_noise", ptr(x.contiguous()), ptr(z.contiguous()), ptr(ts_raw.float().contiguous()), C, P, B * N,
+         ptr(xt), ptr(tgt), ptr(ts), stream())
+    return xt, tgt, ts.to(BF16)
+
+
+def unpatchify(tok, B, N, C, h, w):
+    out = torch.empty(B, N, C, h, w, device=tok.device, dtype=BF16)
+    call("owlk_unpatchify", ptr(tok), C, h * w, B * N, ptr(out), stream())
+    return out
+
+
+def mse(pred, tgt, want_grad=True, grad_scale=1.0):
+    """F.mse_loss (fp32 math on bf16 inputs) + d loss / d pred (bf16)."""
+    n = pred.numel()
+    nb = 1024
+    partial = torch.empty(nb, device=pred.device, dtype=F32)
+    dpred = torch.empty_like(pred) if want_grad else None
+    call("owlk_mse", ptr(pred), ptr(tgt), n, float(2.0 * grad_scale / n), ptr(dpred), ptr(partial), nb, stream())
+    return partial.double().sum().float() / n, dpred
+
+
+def colsum(x, out=None):
+    """fp32 column sums of a 2-D row-major view."""
+    R, N = x.shape
+    if out is None:
+        out = torch.zeros(N, device=x.device, dtype=F32)
+    call("owlk_colsum", ptr(x), int(x.dtype == F32), R, N, x.stride(0), ptr(out), stream())
+    return out
+
+
+def ns_normalize(g, transpose, work=None):
+    """g [b, r, c] (fp32 or bf16) -> X bf16 [b, r, c] or [b, c, r] (transpose) / (||X||_F + 1e-7)."""
+    b, r, c = g.shape
+    x = torch.empty(b, c, r, device=g.device, dtype=BF16) if transpose else torch.empty(b, r, c, device=g.device,
+                                                                                        dtype=BF16)
+    work = torch.empty(b, device=g.device, dtype=F32) if work is None else work
+    g = g.contiguous()
+    call("owlk_ns_normalize", ptr(g), int(g.dtype == F32), r, c, b, int(transpose), ptr(x), ptr(work), stream())
+    return x

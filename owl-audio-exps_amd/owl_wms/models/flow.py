@@ -1,0 +1,64 @@
+"""Shared flow-matching objective pieces (gamerft.py:68-124, audiorft.py:59-93)."""
+import torch
+
+from .. import kernels as K
+from ..nn.fused import FlowLossFn
+
+
+class TorchNoise:
+    """Default noise source: the reference's draw order on the input's device
+    (rand(b) for CFG dropout -> randn(B, S) for timesteps -> randn_like(x))."""
+
+    def rand_b(self, b, device):
+        return torch.rand(b, device=device)
+
+    def ts_raw(self, B, S, device, dtype):
+        return torch.randn(B, S, device=device, dtype=dtype)
+
+    def z(self, x):
+        return torch.randn_like(x)
+
+
+class InjectedNoise:
+    """Parity runs: replay pre-drawn tensors (a dict with rand_b / ts_raw / z)."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def rand_b(self, b, device):
+        return self.d["rand_b"].to(device)
+
+    def ts_raw(self, B, S, device, dtype):
+        return self.d["ts_raw"].to(device=device, dtype=dtype)
+
+    def z(self, x):
+        return self.d["z"].to(device=x.device, dtype=x.dtype)
+
+
+def handle_cfg(has_controls, cfg_prob, noise):
+    """gamerft.py:68-90 (the Python-level comparison syncs the host once, as in the reference)."""
+    if cfg_prob <= 0.0 or has_controls is None:
+        return has_controls
+    frac = has_controls.float().mean()
+    pct_without = 1.0 - frac
+    if pct_without < cfg_prob:
+        needed_frac = (cfg_prob - pct_without) / frac
+        b = has_controls.shape[0]
+        mask = (noise.rand_b(b, has_controls.device) <= needed_frac) & has_controls
+        has_controls = has_controls & (~mask)
+    return has_controls
+
+
+def noised_tokens(x5, noise):
+    """x5 [B, N, C, P...] -> (x_t tokens, target tokens, ts bf16 [B, N], z) via owlk_flow_noise."""
+    B, N = x5.shape[:2]
+    xb = x5.to(torch.bfloat16)
+    ts_raw = noise.ts_raw(B, N, xb.device, torch.bfloat16)
+    z = noise.z(xb)
+    shp = xb.shape
+    xt, tgt, ts = K.flow_noise(xb.reshape(B, N, shp[2], -1, 1), z.reshape(B, N, shp[2], -1, 1), ts_raw)
+    return xt, tgt, ts, z
+
+
+def flow_loss(pred_tok, tgt_tok):
+    return FlowLossFn.apply(pred_tok, tgt_tok)

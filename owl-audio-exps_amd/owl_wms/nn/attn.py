@@ -1,0 +1,186 @@
+"""attn.py (reference: owl_wms/nn/attn.py) -- DiT backbone on libowlk.
+
+``get_block_mask`` returns a :class:`FrameMask` (analytic frame/window/doc description consumed
+by the attention kernels) instead of a dense-evaluated flex BlockMask: same mask semantics
+(attn.py:24-62), O(frames) host work instead of 2 x T^2 predicate evaluations per step.
+
+Training path: ``DiTBlock.forward`` -> ``DiTBlockFn`` (whole block fwd+bwd fused on libowlk).
+Sampling path (``kv_cache`` given): a no-grad functional path with the reference's cache
+semantics (attn.py:86-107): cached K/V prepended, local layers keep the last
+``local_window * tokens_per_frame`` keys when decoding unmasked.
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.utils.checkpoint import checkpoint as torch_checkpoint
+
+from .. import kernels as K
+from .fused import BlockGeometry, DiTBlockFn, adaln, bf16_weight, linear
+from .mlp import MLP
+from .modulation import AdaLN, Gate
+from .rope import get_rope_cls
+
+
+def checkpoint(function, *args, **kwargs):
+    kwargs.setdefault("use_reentrant", False)
+    return torch_checkpoint(function, *args, **kwargs)
+
+
+def get_block_mask(n_tokens, tokens_per_frame, window_len=None, doc_id=None, q_offset=0, is_causal=True,
+                   device="cuda"):
+    """attn.py:24-62 -> FrameMask (Q_LEN = n_tokens - q_offset, KV_LEN = n_tokens)."""
+    assert 0 <= q_offset < n_tokens, "kv cache cannot exceed total tokens"
+    if not is_causal:
+        assert q_offset == 0, "kv caching not supported with bidirectional"
+    arrays = None
+    if doc_id is not None:
+        n_frames = (n_tokens + tokens_per_frame - 1) // tokens_per_frame
+        arrays = K.frame_arrays(doc_id.to(device), n_frames, window_len, is_causal)
+    return K.FrameMask(tokens_per_frame, window_len, is_causal, q_offset, arrays)
+
+
+class Attn(nn.Module):
+    def __init__(self, config, layer_idx, local=False, rope=None):
+        super().__init__()
+        self.config = config
+        self.layer_idx = layer_idx
+        self.n_heads = config.n_heads
+        self.qkv = nn.Linear(config.d_model, 3 * config.d_model)
+        self.out = nn.Linear(config.d_model, config.d_model)
+        # one RoPE table per model (non-persistent buffers, rope.py:40-41), shared by every layer
+        object.__setattr__(self, "rope", rope if rope is not None else
+                           get_rope_cls(getattr(config, "rope_impl", "ortho"))(config))
+        self.local = local
+        self.local_offset = config.local_window * config.tokens_per_frame
+
+    def forward(self, x, block_mask, kv_cache=None):
+        """Stand-alone attention (x already modulated) -- reference API; no-grad cache path."""
+        B, L, d = x.shape
+        H = self.n_heads
+        D = d // H
+        x2 = x.reshape(B * L, d).to(torch.bfloat16).contiguous()
+        qkv = K.gemm(x2, bf16_weight(self.qkv.weight), bias=self.qkv.bias)
+        o = self._attend(qkv, B, L, block_mask, kv_cache)
+        return K.gemm(o.reshape(B * L, d), bf16_weight(self.out.weight), bias=self.out.bias).view(B, L, d)
+
+    def _attend(self, qkv, B, L, block_mask, kv_cache):
+        d = self.config.d_model
+        H = self.n_heads
+        D = d // H
+        offset = kv_cache.get_offset(self.layer_idx) if kv_cache is not None else 0
+        qkr, _ = K.qk_rope_fwd(qkv, H, D, self.rope.cos, self.rope.sin, offset, L)
+        q = qkr.view(B, L, 2 * d)[:, :, :d]
+        k = qkr.view(B, L, 2 * d)[:, :, d:]
+        v = qkv.view(B, L, 3 * d)[:, :, 2 * d:]
+        if offset > 0:
+            old_k, old_v = kv_cache.get(self.layer_idx)
+            k = torch.cat([old_k, k], dim=1)
+            v = torch.cat([old_v, v], dim=1)
+        if kv_cache is not None and kv_cache.should_update:
+            kv_cache.update(k.contiguous(), v.contiguous(), self.layer_idx)
+        if block_mask is None:  # decoding: unmasked over [cache | new] (attn.py:101-107)
+            if self.local:
+                k, v = k[:, -self.local_offset:], v[:, -self.local_offset:]
+            mask = K.FrameMask(1, None, False, 0, None)
+        else:
+            mask = block_mask
+        o, _ = K.attn_fwd(q, k, v, H, D, mask)
+        return o
+
+
+class DiTBlock(nn.Module):
+    def __init__(self, config, layer_idx, local=False, rope=None):
+        super().__init__()
+        dim = config.d_model
+        self.attn = Attn(config, layer_idx, local, rope)
+        self.mlp = MLP(config)
+        self.adaln1 = AdaLN(dim)
+        self.gate1 = Gate(dim)
+        self.adaln2 = AdaLN(dim)
+        self.gate2 = Gate(dim)
+        self.config = config
+
+    def modulation(self, cond):
+        s = F.silu(cond)
+        return self.adaln1.mod(s), self.gate1.mod(s), self.adaln2.mod(s), self.gate2.mod(s)
+
+    def forward(self, x, cond, block_mask, kv_cache=None):
+        if kv_cache is not None:
+            with torch.no_grad():
+                return self._forward_cached(x, cond, block_mask, kv_cache)
+        cfg = self.config
+        ab1, g1, ab2, g2 = self.modulation(cond)
+        H = cfg.n_heads
+        rope = self.attn.rope
+        geo = BlockGeometry(H, cfg.d_model // H, cfg.tokens_per_frame, block_mask, rope.cos, rope.sin, 0)
+        a, m = self.attn, self.mlp
+        return DiTBlockFn.apply(x.to(torch.bfloat16).contiguous(), ab1, g1, ab2, g2, a.qkv.weight, a.qkv.bias,
+                                a.out.weight, a.out.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias, geo)
+
+    def _forward_cached(self, x, cond, block_mask, kv_cache):
+        cfg = self.config
+        d, tpf = cfg.d_model, cfg.tokens_per_frame
+        B, L, _ = x.shape
+        ab1, g1, ab2, g2 = self.modulation(cond)
+        xx = x.reshape(B * L, d).to(torch.bfloat16).contiguous()
+        ab1, ab2 = ab1.reshape(-1, 2 * d), ab2.reshape(-1, 2 * d)
+        h1, _ = K.adaln_fwd(xx, ab1[:, :d], ab1[:, d:], tpf)
+        qkv = K.gemm(h1, bf16_weight(self.attn.qkv.weight), bias=self.attn.qkv.bias)
+        o = self.attn._attend(qkv, B, L, block_mask, kv_cache)
+        x1 = K.gemm(o.reshape(B * L, d), bf16_weight(self.attn.out.weight), bias=self.attn.out.bias,
+                    epi=K.EPI_GATE_RESID, gate=g1.reshape(-1, d), tpf=tpf, resid=xx)
+        h2, _ = K.adaln_fwd(x1, ab2[:, :d], ab2[:, d:], tpf)
+        a_pre = torch.empty(B * L, 4 * d, device=x.device, dtype=torch.bfloat16)
+        a = K.gemm(h2, bf16_weight(self.mlp.fc1.weight), bias=self.mlp.fc1.bias, epi=K.EPI_SILU, aux=a_pre)
+        out = K.gemm(a, bf16_weight(self.mlp.fc2.weight), bias=self.mlp.fc2.bias, epi=K.EPI_GATE_RESID,
+                     gate=g2.reshape(-1, d), tpf=tpf, resid=x1)
+        return out.view(B, L, d)
+
+
+class DiT(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        if not hasattr(config, "local_idx"):
+            config.local_idx = 4
+        self.rope = get_rope_cls(getattr(config, "rope_impl", "ortho"))(config)
+        self.local_layers = [(i % config.local_idx != 0) for i in range(config.n_layers)]
+        self.blocks = nn.ModuleList([DiTBlock(config, i, loc, self.rope) for i, loc in enumerate(self.local_layers)])
+        self.decoding = False
+
+    def enable_decoding(self):
+        self.decoding = True
+
+    def disable_decoding(self):
+        self.decoding = False
+
+    def get_block_mask(self, seq_len, doc_id, window_len, q_offset, device):
+        return get_block_mask(seq_len + q_offset, self.config.tokens_per_frame, window_len, doc_id, q_offset,
+                              self.config.causal, device)
+
+    def forward(self, x, cond, doc_id=None, kv_cache=None, local_block_mask=None, global_block_mask=None):
+        seq_len, device = x.size(1), x.device
+        q_offset = kv_cache.length_at(0) if kv_cache is not None else 0
+        if local_block_mask is None and not self.decoding:
+            local_block_mask = self.get_block_mask(seq_len, doc_id, self.config.local_window, q_offset, device)
+        if global_block_mask is None and not self.decoding:
+            global_block_mask = self.get_block_mask(seq_len, doc_id, getattr(self.config, "global_window", None),
+                                                    q_offset, device)
+        ckpt = self.training and getattr(self.config, "gradient_checkpointing", False) and kv_cache is None
+        for i, block in enumerate(self.blocks):
+            mask = local_block_mask if self.local_layers[i] else global_block_mask
+            x = checkpoint(block, x, cond, mask, kv_cache) if ckpt else block(x, cond, mask, kv_cache)
+        return x
+
+
+class FinalLayer(nn.Module):
+    """attn.py:264-277: proj(silu(AdaLN(x, cond))) with AdaLN + SiLU fused in one kernel."""
+
+    def __init__(self, sample_size, d_model, channels=3, patch_size=1):
+        super().__init__()
+        self.norm = AdaLN(d_model)
+        self.act = nn.SiLU()
+        self.proj = nn.Linear(d_model, channels * patch_size * patch_size)
+
+    def forward(self, x, cond):
+        return linear(self.norm(x, cond, act=True), self.proj.weight, self.proj.bias)

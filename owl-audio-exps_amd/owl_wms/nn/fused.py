@@ -1,0 +1,220 @@
+"""autograd Functions over libowlk: the training hot path of owl_wms on MI355X.
+
+* ``linear``      nn.Linear under bf16 autocast (fp32 params, bf16 activations) -- every
+                  Linear outside the block loop (embeddings, proj_in/out, modulation fcs).
+* ``adaln``       AdaLN / cond_adaln modulate with optional fused SiLU (FinalLayer).
+* ``DiTBlockFn``  one whole DiTBlock (attn.py:116-143) forward + backward:
+                    h1 = AdaLN1(x)                      adaln_fwd
+                    qkv = h1 Wqkv^T + b                 GEMM
+                    q, k = rope(rms(q)), rope(rms(k))   qk_rope_fwd
+                    o = attn(q, k, v)                   attn_fwd (frame mask, no mask tensor)
+                    x1 = x + g1 * (o Wout^T + b)        GEMM + gate/residual epilogue
+                    h2 = AdaLN2(x1)                     adaln_fwd
+                    a = silu(h2 W1^T + b1)              GEMM + SiLU epilogue
+                    x2 = x1 + g2 * (a W2^T + b2)        GEMM + gate/residual epilogue
+                  and the mirrored backward (dX GEMMs with fused SiLU', dW GEMMs straight into
+                  fp32, deterministic flash-attention backward).
+
+Parameters stay fp32 (the reference trains fp32 master weights under autocast); their bf16
+copies are cached on the parameter and refreshed only when its version counter moves (i.e.
+after an optimizer step), not once per micro-step.
+"""
+import torch
+import torch.nn.functional as F
+
+from .. import kernels as K
+
+BF16 = torch.bfloat16
+
+
+def bf16_weight(p, pad_k=0):
+    """Cached bf16 (optionally K-padded) copy of an fp32 parameter."""
+    ent = getattr(p, "_owl_bf16", None)
+    ver = p._version
+    if ent is None or ent[0] != ver or ent[1] != pad_k or ent[2].device != p.device:
+        w = p.detach().to(BF16)
+        if pad_k:
+            w = F.pad(w, (0, pad_k))
+        w = w.contiguous()
+        p._owl_bf16 = (ver, pad_k, w)
+        return w
+    return ent[2]
+
+
+def _pad_k(K_):
+    return (-K_) % 8
+
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shp = x.shape
+        Kd = shp[-1]
+        pad = _pad_k(Kd)
+        x2 = x.reshape(-1, Kd).to(BF16)
+        if pad:
+            x2 = F.pad(x2, (0, pad))
+        x2 = x2.contiguous()
+        wb = bf16_weight(w, pad)
+        y = K.gemm(x2, wb, bias=b)
+        ctx.save_for_backward(x2, w)
+        ctx.pad, ctx.shp, ctx.has_b, ctx.xdtype = pad, shp, b is not None, x.dtype
+        return y.view(*shp[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        N = w.shape[0]
+        dy2 = dy.reshape(-1, N).to(BF16).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wb = bf16_weight(w, ctx.pad)
+            dx = K.gemm(dy2, wb, b_trans=True)
+            if ctx.pad:
+                dx = dx[:, : ctx.shp[-1]]
+            dx = dx.reshape(ctx.shp).to(ctx.xdtype)
+        if ctx.needs_input_grad[1]:
+            dw = K.gemm(dy2, x2, a_trans=True, b_trans=True, out_f32=True)
+            if ctx.pad:
+                dw = dw[:, : ctx.shp[-1]].contiguous()
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = K.colsum(dy2)
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    """bf16-autocast nn.Linear on libowlk (x: [..., K] any float dtype -> [..., N] bf16)."""
+    return LinearFn.apply(x, w, b)
+
+
+class AdaLNFn(torch.autograd.Function):
+    """y = bf16(rms(x)) * (1 + scale[frame]) + shift[frame]  (optionally -> silu(y))."""
+
+    @staticmethod
+    def forward(ctx, x, scale, shift, tpf, act):
+        shp = x.shape
+        d = shp[-1]
+        x2 = x.reshape(-1, d).to(BF16).contiguous()
+        sc2, sh2 = scale.reshape(-1, d), shift.reshape(-1, d)
+        if sc2.stride(1) != 1 or sh2.stride(1) != 1 or sc2.stride(0) != sh2.stride(0):
+            sc2, sh2 = sc2.contiguous(), sh2.contiguous()
+        if act:
+            y, rstd, ya = K.adaln_fwd(x2, sc2, sh2, tpf, act=True)
+        else:
+            (y, rstd), ya = K.adaln_fwd(x2, sc2, sh2, tpf), None
+        ctx.save_for_backward(x2, rstd, sc2, y if act else None)
+        ctx.tpf, ctx.shp, ctx.act, ctx.mshape = tpf, shp, act, scale.shape
+        return (ya if act else y).view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, rstd, sc2, ypre = ctx.saved_tensors
+        d = x2.shape[1]
+        dy2 = dy.reshape(-1, d).to(BF16).contiguous()
+        dx, dmod = K.adaln_bwd(dy2, x2, rstd, sc2, ctx.tpf, ypre=ypre if ctx.act else None)
+        return dx.view(ctx.shp), dmod[:, :d].reshape(ctx.mshape), dmod[:, d:].reshape(ctx.mshape), None, None
+
+
+def adaln(x, scale, shift, tpf, act=False):
+    return AdaLNFn.apply(x, scale, shift, tpf, act)
+
+
+class BlockGeometry:
+    """Static per-forward data of a DiT block: heads, frame mask, RoPE tables."""
+
+    def __init__(self, n_heads, head_dim, tpf, mask, cos, sin, tab_off=0):
+        self.H, self.D, self.tpf, self.mask = n_heads, head_dim, tpf, mask
+        self.cos, self.sin, self.tab_off = cos, sin, tab_off
+
+
+class DiTBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ab1, g1, ab2, g2, wqkv, bqkv, wout, bout, w1, b1, w2, b2, geo):
+        B, T, d = x.shape
+        M = B * T
+        H, D, tpf = geo.H, geo.D, geo.tpf
+        xx = x.reshape(M, d)
+        a1, a2 = ab1.reshape(-1, 2 * d), ab2.reshape(-1, 2 * d)
+        gg1, gg2 = g1.reshape(-1, d), g2.reshape(-1, d)
+
+        h1, r1 = K.adaln_fwd(xx, a1[:, :d], a1[:, d:], tpf)
+        qkv = K.gemm(h1, bf16_weight(wqkv), bias=bqkv)
+        qkr, rq = K.qk_rope_fwd(qkv, H, D, geo.cos, geo.sin, geo.tab_off, T)
+        q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
+        o, lse = K.attn_fwd(q3, k3, qkv.view(B, T, 3 * d)[:, :, 2 * d:], H, D, geo.mask)
+        o = o.view(M, d)
+        y1 = torch.empty(M, d, device=x.device, dtype=BF16)
+        x1 = K.gemm(o, bf16_weight(wout), bias=bout, epi=K.EPI_GATE_RESID, aux=y1, gate=gg1, tpf=tpf, resid=xx)
+        h2, r2 = K.adaln_fwd(x1, a2[:, :d], a2[:, d:], tpf)
+        a_pre = torch.empty(M, w1.shape[0], device=x.device, dtype=BF16)
+        a = K.gemm(h2, bf16_weight(w1), bias=b1, epi=K.EPI_SILU, aux=a_pre)
+        y2 = torch.empty(M, d, device=x.device, dtype=BF16)
+        out = K.gemm(a, bf16_weight(w2), bias=b2, epi=K.EPI_GATE_RESID, aux=y2, gate=gg2, tpf=tpf, resid=x1)
+
+        ctx.save_for_backward(xx, a1, gg1, a2, gg2, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2,
+                              r2, a_pre, a, y2)
+        ctx.geo, ctx.shape = geo, (B, T, d)
+        return out.view(B, T, d)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (xx, a1, gg1, a2, gg2, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2, r2, a_pre, a,
+         y2) = ctx.saved_tensors
+        geo = ctx.geo
+        B, T, d = ctx.shape
+        M = B * T
+        H, D, tpf = geo.H, geo.D, geo.tpf
+        dx2 = dout.reshape(M, d).to(BF16).contiguous()
+
+        # ---- MLP branch
+        dy2, dg2, dbf2 = K.gate_bwd(dx2, y2, gg2, tpf)
+        db2 = dbf2.sum(0)
+        dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre)
+        dw2 = K.gemm(dy2, a, a_trans=True, b_trans=True, out_f32=True)
+        db1 = K.colsum(dapre)
+        dw1 = K.gemm(dapre, h2, a_trans=True, b_trans=True, out_f32=True)
+        dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
+        del dapre
+        dx1, dmod2 = K.adaln_bwd(dh2, x1, r2, a2[:, :d], tpf, dres=dx2)
+        del dh2
+
+        # ---- attention branch
+        dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf)
+        dbout = dbf1.sum(0)
+        do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
+        dwout = K.gemm(dy1, o, a_trans=True, b_trans=True, out_f32=True)
+        del dy1
+        dqkv = torch.empty(M, 3 * d, device=xx.device, dtype=BF16)
+        dqkr = torch.empty(M, 2 * d, device=xx.device, dtype=BF16)
+        q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
+        dq3, dk3 = dqkr.view(B, T, 2 * d)[:, :, :d], dqkr.view(B, T, 2 * d)[:, :, d:]
+        K.attn_bwd(q3, k3, qkv.view(B, T, 3 * d)[:, :, 2 * d:], o.view(B, T, d), do.view(B, T, d), lse, H, D,
+                   geo.mask, dq3, dk3, dqkv.view(B, T, 3 * d)[:, :, 2 * d:])
+        del do
+        K.qk_rope_bwd(dqkr, qkv, rq, H, D, geo.cos, geo.sin, dqkv, geo.tab_off, T)
+        del dqkr
+        dbqkv = K.colsum(dqkv)
+        dwqkv = K.gemm(dqkv, h1, a_trans=True, b_trans=True, out_f32=True)
+        dh1 = K.gemm(dqkv, bf16_weight(wqkv), b_trans=True)
+        del dqkv
+        dx, dmod1 = K.adaln_bwd(dh1, xx, r1, a1[:, :d], tpf, dres=dx1)
+
+        nf = M // tpf
+        return (dx.view(B, T, d), dmod1.view(B, nf // B, 2 * d), dg1.view(B, nf // B, d),
+                dmod2.view(B, nf // B, 2 * d), dg2.view(B, nf // B, d),
+                dwqkv, dbqkv, dwout, dbout, dw1, db1, dw2, db2, None)
+
+
+class FlowLossFn(torch.autograd.Function):
+    """F.mse_loss(pred_tok, tgt_tok) with the gradient produced by the same kernel."""
+
+    @staticmethod
+    def forward(ctx, pred, tgt):
+        loss, dpred = K.mse(pred.contiguous(), tgt.contiguous(), want_grad=pred.requires_grad)
+        ctx.save_for_backward(dpred)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dpred,) = ctx.saved_tensors
+        return dpred * g.to(dpred.dtype), None

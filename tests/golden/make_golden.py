@@ -289,8 +289,25 @@ def gen_audio_traj():
     return out
 
 
+def gen_schema():
+    """state_dict key -> shape of the reference models (checkpoint compatibility)."""
+    out = {}
+    for tag, cfg in [("tiny", tiny_video_cfg()),
+                     ("dit_v4", tiny_video_cfg(channels=128, n_layers=16, n_heads=24, d_model=1536, n_frames=1536,
+                                               local_window=16))]:
+        m = r_gamerft.GameRFT(cfg)
+        out[tag] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+        del m
+    m = r_audiorft.AudioRFT(audio_cfg())
+    out["audio_tiny"] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    return out
+
+
 def main():
     torch.manual_seed(0)
+    import json
+    with open(os.path.join(HERE, "schema.json"), "w") as f:
+        json.dump(gen_schema(), f)
     ops = gen_ops()
     torch.save(ops, os.path.join(HERE, "ops.pt"))
     gr = gen_gamerft()
