@@ -1,0 +1,209 @@
+"""Benchmark: dit_v4 training step on MI355X (BASELINE.json metric).
+
+A step = one optimizer step of configs/dit_v4.yml at global batch 16 (target_batch_size): each of
+the N ranks runs 16/N micro-steps of fwd+bwd on one synthetic 1536-frame x 8x8 latent sample
+(98,304 tokens), the bucketed RCCL gradient all-reduce overlapped with the last backward, then
+the Muon (libowlk Newton-Schulz) + AdamW step and the EMA update.  Strong scaling: total work per
+step is fixed as N grows.  value = 16 * 98,304 * K tokens / (max-over-ranks wall time of K steps).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Extra fields: roofline (dominant kernel, HIP events on the launch stream, algorithmic FLOPs),
+cpu_baseline (the fp32 CPU oracle at dit_v4 width/depth on 1,024 tokens, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "owl-audio-exps_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "latent-tokens/sec/GPU (fwd+bwd) DiT-v4 bf16; 1/2/4/8-GPU scaling"
+PEAK_BF16 = 2.5e15           # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: Peak BF16 MFMA)
+PEAK_HBM = 8.0e12
+FLOP_PER_TOKEN = 6.596e9     # dit_v4 fwd+bwd algorithmic FLOPs per token
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(steps=3):
+    """fp32 CPU oracle (oracle/ref_model.py) at dit_v4 width/depth, 16 frames = 1,024 tokens."""
+    from types import SimpleNamespace
+
+    from oracle import ref_model as M
+    from oracle.params import det_tensor
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = min(ncpu, 16)
+    torch.set_num_threads(cores)
+    cfg = SimpleNamespace(model_id="game_rft", sample_size=8, channels=128, n_layers=16, n_heads=24, d_model=1536,
+                          tokens_per_frame=64, n_buttons=11, cfg_prob=0.1, n_frames=16, causal=True, uncond=False,
+                          backbone="dit", has_audio=False, rope_impl="motion", rope_ats_delta=2.0, local_window=16,
+                          global_window=None)
+    torch.manual_seed(0)
+    model = M.GameRFT(cfg).train()
+    B, n = 1, 16
+    x = det_tensor((B, n, 128, 8, 8), 1)
+    mouse, btn = det_tensor((B, n, 2), 2), (det_tensor((B, n, 11), 3) > 0).float()
+    doc = torch.zeros(B, n, dtype=torch.long)
+    noise = {"rand_b": torch.tensor([0.5]), "ts_raw": det_tensor((B, n), 4), "z": det_tensor((B, n, 128, 8, 8), 5)}
+    times = []
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        loss, _, _ = model(x, mouse, btn, doc, noise)
+        loss.backward()
+        times.append(time.perf_counter() - t0)
+        model.zero_grad(set_to_none=True)
+        log(f"[cpu_baseline] step {i} {times[-1]:.2f}s")
+    t = statistics.median(times[1:])
+    return {"value": round(1024 / t, 2), "unit": "latent-tokens/s", "cores": cores, "kind": "port",
+            "sample": f"oracle fp32 CPU fwd+bwd, dit_v4 width/depth (16 L, d1536, 24 H), 16 frames = 1,024 tokens, "
+                      f"batch 1, median of {steps} steps after 1 warm-up ({t:.2f} s/step); different (shorter) "
+                      f"sequence than the GPU workload"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--global-batch", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=1536)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
+        os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+
+    from owl_wms import _lib
+    from owl_wms.configs import Config
+    from owl_wms.data import synthetic_video_batch
+    from owl_wms.models import get_model_cls
+    from owl_wms.muon import init_muon
+    from owl_wms.utils.grad_reducer import EMA, GradReducer
+
+    cfg = Config.from_yaml(os.path.join(REPO, "configs", "dit_v4.yml"))
+    mc = cfg.model
+    mc.n_frames = args.frames
+    tokens = mc.n_frames * mc.tokens_per_frame
+    accum = max(1, args.global_batch // world)
+    torch.manual_seed(0)
+    model = get_model_cls(mc.model_id)(mc).cuda().train()
+    if world > 1:
+        with torch.no_grad():
+            for p in model.parameters():
+                dist.broadcast(p, 0)
+    opt = init_muon(model, rank=rank, world_size=world, **cfg.train.opt_kwargs)
+    ema = EMA(model, beta=0.999)
+    red = GradReducer(model.parameters(), world_size=world)
+    batches = [[t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234 + rank * 97 + i)] for i in range(2)]
+    vae_scale = cfg.train.vae_scale
+
+    def micro(i, sync):
+        vid, mouse, btn, doc = batches[i % 2]
+        red.begin(sync)
+        loss = model(vid / vae_scale, mouse, btn, doc) / accum
+        loss.backward()
+        red.finish()
+        return loss
+
+    def step():
+        for i in range(accum):
+            micro(i, i == accum - 1)
+        opt.step()
+        red.zero_grad()
+        ema.update()
+
+    for w in range(args.warmup):
+        t0 = time.time()
+        step()
+        torch.cuda.synchronize()
+        log(f"[bench] warmup {w} {time.time() - t0:.2f}s")
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step()
+        if rank == 0:
+            log(f"[bench] step {s} issued at {time.perf_counter() - t0:.2f}s")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_per_step = elapsed / args.steps * 1e3
+    total_tokens = args.global_batch * tokens * args.steps
+    value = total_tokens / elapsed
+
+    # ---- roofline of the dominant kernel: one extra micro-step with HIP events around every launch
+    roof, kernels = None, None
+    if not args.no_profile:
+        torch.cuda.synchronize()
+        _lib.profile_begin()
+        micro(0, False)
+        prof = _lib.profile_end()
+        red.zero_grad()
+        kernels = sorted(prof.items(), key=lambda kv: -kv[1][1])
+        tot_ms = sum(v[1] for v in prof.values())
+        # group launches by kernel symbol (rocprof granularity): strip the shape suffix
+        sym = {}
+        for k, (n, ms, fl) in prof.items():
+            s = k.split("[")[0] if k.startswith("gemm") else k.split("[")[0]
+            a = sym.setdefault(s, [0, 0.0, 0.0])
+            a[0] += n
+            a[1] += ms
+            a[2] += fl
+        dom, (n, ms, fl) = max(sym.items(), key=lambda kv: kv[1][1])
+        achieved = fl / (ms / 1e3) if ms > 0 else 0.0
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
+                "launches_per_microstep": n, "avg_launch_ms": round(ms / n, 4),
+                "share_of_microstep_kernel_time": round(ms / tot_ms, 3)}
+        if rank == 0:
+            log("[bench] per-kernel time in one micro-step (ms):")
+            for k, (n, ms_, fl_) in kernels[:40]:
+                log(f"  {k:60s} n={n:3d} {ms_:9.3f} ms  {fl_ / max(ms_, 1e-9) / 1e9:8.1f} TF/s")
+            log(f"  total kernel time {tot_ms:.1f} ms")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "latent-tokens/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 1),
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (random latents of the dit_v4 shape, random-init weights)",
+               "config": {"workload": f"configs/dit_v4.yml training step: global batch {args.global_batch} x "
+                                      f"{mc.n_frames} frames x 8x8 latents ({tokens} tokens/sample), fwd+bwd + "
+                                      f"RCCL grad all-reduce + Muon/AdamW step + EMA",
+                          "model": "dit_v4 (16 L, d1536, 24 H, 704.9M params)", "global_batch": args.global_batch,
+                          "seq_len": tokens, "parallelism": f"dp{world}"},
+               "tokens_per_s_per_gpu": round(value / world, 1),
+               "step_mfma_frac": round(value * FLOP_PER_TOKEN / world / PEAK_BF16, 4),
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

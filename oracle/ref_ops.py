@@ -157,8 +157,14 @@ def sincos(x, dim, theta=300.0, mult=1000.0):
 NS_COEF = (3.4445, -4.7750, 2.0315)
 
 
-def newton_schulz5(G, steps=5):
-    """muon.py:11-38: quintic Newton-Schulz in bf16 (eager rounding order)."""
+def newton_schulz5(G, steps=5, order="eager"):
+    """muon.py:11-38: quintic Newton-Schulz in bf16.
+
+    order="eager": the reference's eager rounding, B = bf16(b*A) + bf16(bf16(c*A) @ A).
+    order="epilogue": the same math with the scalar applied after the product,
+    B = bf16(b*A) + bf16(c * bf16(A @ A^T)), as libowlk's AXPBY GEMM epilogue rounds it.
+    (bf16 NS is chaotic in its rounding order: the two orders differ by ~2.7% rel-L2.)
+    """
     a, b, c = NS_COEF
     X = G.bfloat16()
     tr = G.size(-2) > G.size(-1)
@@ -167,7 +173,7 @@ def newton_schulz5(G, steps=5):
     X = X / (X.norm(dim=(-2, -1), keepdim=True) + 1e-7)
     for _ in range(steps):
         A = X @ X.mT
-        B = b * A + c * A @ A
+        B = b * A + c * A @ A if order == "eager" else b * A + c * (A @ A.mT)
         X = a * X + B @ X
     if tr:
         X = X.mT

@@ -58,10 +58,38 @@ def exported_symbols():
     return ["owlk_last_error", "owlk_version", "owlk_device_ok"] + list(_SIGS)
 
 
-def call(name, *args):
+_profile = None  # list of (key, flops, start_event, end_event) while a profile window is open
+
+
+def profile_begin():
+    global _profile
+    _profile = []
+
+
+def profile_end():
+    """-> {key: (launches, total_ms, total_flops)} for the calls made since profile_begin()."""
+    global _profile
+    torch.cuda.synchronize()
+    out = {}
+    for key, flops, e0, e1 in _profile or []:
+        n, ms, fl = out.get(key, (0, 0.0, 0.0))
+        out[key] = (n + 1, ms + e0.elapsed_time(e1), fl + (flops or 0.0))
+    _profile = None
+    return out
+
+
+def call(name, *args, key=None, flops=None):
+    prof = _profile
+    if prof is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {lib().owlk_last_error().decode()}")
+    if prof is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        prof.append((key or name, flops() if callable(flops) else flops, e0, e1))
 
 
 def ptr(t):

@@ -40,6 +40,7 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
             assert t.shape == (M, N) and t.stride(1) == 1 and t.dtype == BF16, nm
     if gate is not None:
         assert gate.dim() == 2 and gate.shape[1] == N and gate.stride(1) == 1 and gate.shape[0] * tpf >= M
+    tile = 64 if ((M + 127) // 128) * ((N + 127) // 128) < 512 else 128
     call("owlk_gemm", M, N, K, 1,
          ptr(A), A.stride(0), 0, int(a_trans),
          ptr(B), B.stride(0), 0, int(b_trans),
@@ -48,7 +49,8 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
          ptr(aux), aux.stride(0) if aux is not None else 0, 0,
          ptr(gate), gate.stride(0) if gate is not None else 0, 0, int(tpf),
          ptr(resid), resid.stride(0) if resid is not None else 0, 0,
-         stream())
+         stream(), key=f"gemm<{tile},{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
+         flops=lambda: 2.0 * M * N * K)
     return out
 
 
@@ -189,7 +191,7 @@ def attn_fwd(q, k, v, H, D, mask, scale=None, o=None):
     call("owlk_attn_fwd", ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
          ptr(v), v.stride(1), v.stride(0), ptr(o), o.stride(1), o.stride(0), ptr(lse), B, H, Lq, Lkv, D,
          float(scale), mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), mask.q_offset,
-         *mask.args()[3:], stream())
+         *mask.args()[3:], stream(), key=f"attn_fwd[w{mask.window}]", flops=lambda: 4.0 * D * H * B * mask_pairs(mask, Lq, Lkv))
     return o, lse
 
 
@@ -206,7 +208,23 @@ def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
          ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
          ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),
          ptr(dv), dv.stride(1), dv.stride(0), B, H, L, L, D, float(scale),
-         mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), *mask.args()[3:], stream())
+         mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), *mask.args()[3:], stream(),
+         key=f"attn_bwd[w{mask.window}]", flops=lambda: 8.0 * D * H * B * mask_pairs(mask, L, L))
+
+
+def mask_pairs(mask, Lq, Lkv):
+    """Allowed (query, key) pairs per (batch, head) of a doc-free causal frame mask (SURVEY §8(d)
+    counts algorithmic FLOPs over allowed pairs only).  Docs are ignored (upper bound)."""
+    tpf, w = mask.tpf, mask.window
+    nfq = (Lq + tpf - 1) // tpf
+    off = mask.q_offset // tpf
+    tot = 0
+    if not mask.causal:
+        return float(Lq) * Lkv if w is None else float(Lq) * min(Lkv, (2 * w - 1) * tpf)
+    for f in range(off, off + nfq):
+        nk = (f + 1) if w is None else min(f + 1, w)
+        tot += nk
+    return float(tot) * tpf * tpf
 
 
 def flow_noise(x, z, ts_raw):

@@ -230,13 +230,14 @@ def test_newton_schulz_matches_oracle(shape):
     from conftest import golden
     from owl_wms.muon import newton_schulz_bf16
     ops = golden("ops.pt")
-    g = ops[f"ns.{shape[0]}x{shape[1]}.g"].to(DEV)
-    y = newton_schulz_bf16(g[None])[0]
-    ref = ops[f"ns.{shape[0]}x{shape[1]}.y"]
-    # bf16 Newton-Schulz is chaotic in its rounding order: two valid CPU orders of the same eager
-    # expression (c*(A@A) vs (c*A)@A) already differ by 2.7% rel-L2 (measured), so the bar is 4%
+    g = ops[f"ns.{shape[0]}x{shape[1]}.g"]
+    y = newton_schulz_bf16(g.to(DEV)[None])[0].float().cpu()
+    # (1) kernel parity: the oracle evaluated in the kernel's rounding order (AXPBY epilogue)
+    mine = R.newton_schulz5(g, order="epilogue").float()
+    assert rel(y, mine) < 1e-2
+    # (2) vs the reference's own output: bf16 NS is chaotic in rounding order (the oracle's two
+    #     orders differ by ~2.7% rel-L2 on these inputs), so 4% and the same singular spectrum
+    ref = ops[f"ns.{shape[0]}x{shape[1]}.y"].float()
     assert rel(y, ref) < 4e-2
-    assert (y.float().cpu() - ref.float()).abs().max() < 0.05
-    # and the defining property: singular values pushed into ~[0.5, 1.5]
-    s = torch.linalg.svdvals(y.float().cpu())
-    assert s.min() > 0.3 and s.max() < 1.6
+    sv, sr = torch.linalg.svdvals(y), torch.linalg.svdvals(ref)
+    assert (sv - sr).abs().max() < 0.05
