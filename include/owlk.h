@@ -85,6 +85,19 @@ int owlk_attn_bwd(const void* q, long ldq, long sqb, const void* k, long ldk, lo
                   void* dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim,
                   float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
                   const int* run_start, const int* doc, long fstride, void* stream);
+/* the two phases of owlk_attn_bwd separately: dK/dV (key-owner sweep) and dQ (query-owner sweep) */
+int owlk_attn_bwd_dkdv(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                       long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
+                       const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb,
+                       void* dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim,
+                       float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
+                       const int* run_start, const int* doc, long fstride, void* stream);
+int owlk_attn_bwd_dq(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                     long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
+                     const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb,
+                     void* dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim,
+                     float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
+                     const int* run_start, const int* doc, long fstride, void* stream);
 
 /* ---- Flow-matching noise + patchify (gamerft.py:92-95,107-108,52): x, z [BN, C, P] bf16,
  *   ts_raw [BN] fp32 (bf16-valued randn) -> xt, tgt token-major [BN*P, C]; ts_out = bf16 sigmoid */

@@ -44,7 +44,10 @@ DEV void store_rowT(bf16* dst, const f32x16 (&acc)[2], float mul, int h) {
 }
 
 // ======================================================================== dK, dV
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_k(BwdP p) {
+#ifndef OWLK_DKDV_WAVES
+#define OWLK_DKDV_WAVES 2  // waves per SIMD the register allocation must allow
+#endif
+__global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) {
   constexpr int TILE = TL * D * 2;                     // 8 KiB
   constexpr int BUF = 2 * TILE + 2 * TL * 4;           // Q | dO | lse2 | delta
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -309,12 +312,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(BwdP p) {
 
 }  // namespace
 
-extern "C" int owlk_attn_bwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
-                             long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
-                             const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb,
-                             void* dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim,
-                             float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
-                             const int* run_start, const int* doc, long fstride, void* stream) {
+static int attn_bwd_impl(int phases, const void* q, long ldq, long sqb, const void* k, long ldk, long skb,
+                         const void* v, long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
+                         const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb, void* dv,
+                         long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim, float scale, long tpf,
+                         int window, int causal, const int* kv_lo, const int* q_hi, const int* run_start,
+                         const int* doc, long fstride, void* stream) {
   OWLK_REQUIRE(head_dim == D, "attn_bwd: head_dim %d not built (64 only)", head_dim);
   OWLK_REQUIRE(tpf > 0 && Lq > 0 && Lkv > 0 && B > 0 && H > 0 && Lq == Lkv, "attn_bwd: training shapes only");
   OWLK_REQUIRE(!doc || run_start, "attn_bwd: doc mask needs run_start");
@@ -332,10 +335,29 @@ extern "C" int owlk_attn_bwd(const void* q, long ldq, long sqb, const void* k, l
   p.scale_log2 = scale * LOG2E;
   p.m = owlk_make_mask(tpf, window, causal, 0, Lkv, kv_lo, q_hi, run_start, doc, fstride);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256), 0,
-                     s, p);
-  if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
-  hipLaunchKernelGGL(attn_bwd_dq_k, dim3((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256), 0, s,
-                     p);
-  return owlk::check_launch("attn_bwd_dq");
+  if (phases & 1) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256),
+                       0, s, p);
+    if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
+  }
+  if (phases & 2) {
+    hipLaunchKernelGGL(attn_bwd_dq_k, dim3((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256), 0,
+                       s, p);
+    if (int e = owlk::check_launch("attn_bwd_dq")) return e;
+  }
+  return 0;
 }
+
+#define OWLK_BWD_ARGS                                                                                            \
+  const void *q, long ldq, long sqb, const void *k, long ldk, long skb, const void *v, long ldv, long svb,      \
+      const void *dout, long ldo, long sob, const float *lse, const float *delta, void *dq, long lddq, long sdqb, \
+      void *dk, long lddk, long sdkb, void *dv, long lddv, long sdvb, long B, int H, long Lq, long Lkv,          \
+      int head_dim, float scale, long tpf, int window, int causal, const int *kv_lo, const int *q_hi,            \
+      const int *run_start, const int *doc, long fstride, void *stream
+#define OWLK_BWD_FWD                                                                                          \
+  q, ldq, sqb, k, ldk, skb, v, ldv, svb, dout, ldo, sob, lse, delta, dq, lddq, sdqb, dk, lddk, sdkb, dv, lddv, \
+      sdvb, B, H, Lq, Lkv, head_dim, scale, tpf, window, causal, kv_lo, q_hi, run_start, doc, fstride, stream
+
+extern "C" int owlk_attn_bwd(OWLK_BWD_ARGS) { return attn_bwd_impl(3, OWLK_BWD_FWD); }
+extern "C" int owlk_attn_bwd_dkdv(OWLK_BWD_ARGS) { return attn_bwd_impl(1, OWLK_BWD_FWD); }
+extern "C" int owlk_attn_bwd_dq(OWLK_BWD_ARGS) { return attn_bwd_impl(2, OWLK_BWD_FWD); }

@@ -144,39 +144,40 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
           st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[kb], 0, 0, 0);
         }
       }
-      // mask + scale into the log2 domain
+      // mask, row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
       float tmax = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float sv = st[kb][r] * p.scale_log2;
           if (kind == TILE_PARTIAL) {
             const long key = c0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (key >= p.Lkv || my_q >= p.Lq || !allowed(m, b, my_fq, frame_of(m, key))) sv = -INFINITY;
+            if (key >= p.Lkv || my_q >= p.Lq || !allowed(m, b, my_fq, frame_of(m, key))) st[kb][r] = -INFINITY;
           }
-          st[kb][r] = sv;
-          tmax = fmaxf(tmax, sv);
+          tmax = fmaxf(tmax, st[kb][r]);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(mrow, tmax);
-      const float msafe = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = __builtin_amdgcn_exp2f(mrow - msafe);
+      const float mc = mnew == -INFINITY ? 0.f : mnew * p.scale_log2;
+      if (__any(mnew > mrow)) {  // some row's max moved: rescale l and O (exactly)
+        const float alpha = __builtin_amdgcn_exp2f(mrow * p.scale_log2 - mc);
+        lrow *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      }
       mrow = mnew;
       float psum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(st[kb][r] - msafe);
+          const float pv = __builtin_amdgcn_exp2f(fmaf(st[kb][r], p.scale_log2, -mc));
           st[kb][r] = pv;
           psum += pv;
         }
-      lrow = lrow * alpha + psum;
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+      lrow += psum;
 
       // O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
@@ -221,7 +222,8 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
         for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[db][4 * gq + e] * inv);
         *(bf16x4*)(O + 32 * db + 8 * gq + 4 * h) = v4;
       }
-    if (h == 0) p.lse[(b * p.H + head) * p.Lq + my_q] = ltot > 0.f ? (mrow + __log2f(ltot)) * LN2 : -INFINITY;
+    if (h == 0)
+      p.lse[(b * p.H + head) * p.Lq + my_q] = ltot > 0.f ? mrow * p.scale_log2 * LN2 + __logf(ltot) : -INFINITY;
   }
 }
 

@@ -25,6 +25,10 @@ _SIGS = {
     "owlk_attn_delta": [P, P, L, L, L, I, I, P, P],
     "owlk_attn_bwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I, I,
                       P, P, P, P, L, P],
+    "owlk_attn_bwd_dkdv": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I,
+                           I, P, P, P, P, L, P],
+    "owlk_attn_bwd_dq": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I, I,
+                         P, P, P, P, L, P],
     "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
     "owlk_unpatchify": [P, I, I, L, P, P],
     "owlk_mse": [P, P, L, F, P, P, I, P],

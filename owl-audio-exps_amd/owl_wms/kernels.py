@@ -204,12 +204,17 @@ def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
     delta = torch.empty(B, H, L, device=q.device, dtype=F32)
     assert o.is_contiguous() and do.is_contiguous() and o.shape == do.shape
     call("owlk_attn_delta", ptr(o), ptr(do), o.stride(1), B, L, H, D, ptr(delta), stream())
-    call("owlk_attn_bwd", ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
-         ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
-         ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),
-         ptr(dv), dv.stride(1), dv.stride(0), B, H, L, L, D, float(scale),
-         mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), *mask.args()[3:], stream(),
-         key=f"attn_bwd[w{mask.window}]", flops=lambda: 8.0 * D * H * B * mask_pairs(mask, L, L))
+    args = (ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
+            ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
+            ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),
+            ptr(dv), dv.stride(1), dv.stride(0), B, H, L, L, D, float(scale),
+            mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), *mask.args()[3:], stream())
+    # algorithmic FLOPs: dV, dP, dK belong to the key-owner sweep, dQ to the other;
+    # the dq kernel's recomputed S and dP are not counted
+    call("owlk_attn_bwd_dkdv", *args, key=f"attn_bwd_dkdv[w{mask.window}]",
+         flops=lambda: 6.0 * D * H * B * mask_pairs(mask, L, L))
+    call("owlk_attn_bwd_dq", *args, key=f"attn_bwd_dq[w{mask.window}]",
+         flops=lambda: 2.0 * D * H * B * mask_pairs(mask, L, L))
 
 
 def mask_pairs(mask, Lq, Lkv):

@@ -1,0 +1,67 @@
+"""Time the attention kernels at the dit_v4 shape (1 x 24 heads x 98,304 tokens, D 64).
+
+    python tools/attn_bench.py [--frames 1536] [--iters 5]
+Reports ms per launch and algorithmic TF/s (allowed pairs only).
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "owl-audio-exps_amd")]
+import torch  # noqa: E402
+
+from owl_wms import _lib  # noqa: E402
+from owl_wms import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1536)
+    ap.add_argument("--iters", type=int, default=5)
+    args = ap.parse_args()
+    H, D, tpf = 24, 64, 64
+    L = args.frames * tpf
+    torch.manual_seed(0)
+    qkv = torch.randn(1, L, 3 * H * D, device="cuda", dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, :H * D], qkv[:, :, H * D:2 * H * D], qkv[:, :, 2 * H * D:]
+    do = torch.randn(1, L, H * D, device="cuda", dtype=torch.bfloat16)
+    dq, dk, dv = (torch.empty(1, L, H * D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    for window in (None, 16):
+        mask = K.FrameMask(tpf, window)
+        pairs = K.mask_pairs(mask, L, L) * H
+        o, lse = K.attn_fwd(q, k, v, H, D, mask)
+        delta = torch.empty(1, H, L, device="cuda", dtype=torch.float32)
+        _lib.call("owlk_attn_delta", _lib.ptr(o), _lib.ptr(do), o.stride(1), 1, L, H, D, _lib.ptr(delta),
+                  _lib.stream())
+        args_b = (_lib.ptr(q), q.stride(1), q.stride(0), _lib.ptr(k), k.stride(1), k.stride(0), _lib.ptr(v),
+                  v.stride(1), v.stride(0), _lib.ptr(do), do.stride(1), do.stride(0), _lib.ptr(lse),
+                  _lib.ptr(delta), _lib.ptr(dq), dq.stride(1), dq.stride(0), _lib.ptr(dk), dk.stride(1),
+                  dk.stride(0), _lib.ptr(dv), dv.stride(1), dv.stride(0), 1, H, L, L, D, D ** -0.5, tpf,
+                  0 if window is None else window, 1, None, None, None, None, 0, _lib.stream())
+        t_f = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o), args.iters)
+        t_kv = timeit(lambda: _lib.call("owlk_attn_bwd_dkdv", *args_b), args.iters)
+        t_q = timeit(lambda: _lib.call("owlk_attn_bwd_dq", *args_b), args.iters)
+        print(f"window={window}: pairs/head={pairs / H:.4e}")
+        print(f"  fwd   {t_f:8.3f} ms  {4 * D * pairs / t_f / 1e9:7.1f} TF/s (4 D pairs)")
+        print(f"  dkdv  {t_kv:8.3f} ms  {6 * D * pairs / t_kv / 1e9:7.1f} TF/s alg (6 D pairs; 8 D executed: "
+              f"{8 * D * pairs / t_kv / 1e9:.1f})")
+        print(f"  dq    {t_q:8.3f} ms  {2 * D * pairs / t_q / 1e9:7.1f} TF/s alg (2 D pairs; 6 D executed: "
+              f"{6 * D * pairs / t_q / 1e9:.1f})")
+        print(f"  bwd   {t_kv + t_q:8.3f} ms  {8 * D * pairs / (t_kv + t_q) / 1e9:7.1f} TF/s alg", flush=True)
+
+
+if __name__ == "__main__":
+    main()
