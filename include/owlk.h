@@ -28,7 +28,9 @@ int owlk_device_ok(void);
  *       2 GATE_RESID aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m / tpf, n] * y))
  *       3 DSILU      C = bf16(bf16(acc) * silu'(aux))
  *       4 AXPBY      C = bf16(bf16(alpha * bf16(acc)) + bf16(beta * aux))
- *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes. */
+ *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes.
+ *   fp32 STORE with beta == 1 and K >= 8192 onto a small output (weight gradients) splits K over
+ *   workgroups and combines with fp32 atomics: C must hold the accumulation base (e.g. zeros). */
 int owlk_gemm(long M, long N, long K, long batch,
               const void* A, long lda, long sA, int a_trans,
               const void* B, long ldb, long sB, int b_trans,

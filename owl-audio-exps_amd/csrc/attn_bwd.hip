@@ -12,6 +12,8 @@
 //          lane), dQ^T += K^T dS^T with K^T fragments through ds_read_b64_tr_b16.
 #include "attn_common.hpp"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int D = 64;
@@ -142,8 +144,12 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
     int kind = TILE_EMPTY;
     if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
     if (kind == TILE_FULL && (q0 + TL > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
+    kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {
+      const bool masked = kind == TILE_PARTIAL;
+      unsigned long long bits = ~0ull;
+      if (masked) bits = tile_bits(m, b, my_k, my_k < p.Lkv, q0, p.Lq, false);
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         f32x16 st = f32x16{}, dp = f32x16{};
@@ -160,11 +166,8 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g4 + e;
-            float pv = __builtin_amdgcn_exp2f(st[r] * p.scale_log2 - L[e]);
-            if (kind == TILE_PARTIAL) {
-              const long qi = q0 + rowb + e;
-              if (qi >= p.Lq || my_k >= p.Lkv || !allowed(m, b, frame_of(m, qi + m.q_offset), my_fk)) pv = 0.f;
-            }
+            float pv = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L[e]));
+            if (masked && !((bits >> (rowb + e)) & 1ull)) pv = 0.f;
             st[r] = pv;
             dp[r] = pv * (dp[r] - Dl[e]);
           }
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 }
 
 // ======================================================================== dQ
-__global__ __launch_bounds__(256) void attn_bwd_dq_k(BwdP p) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
   constexpr int TILE = TL * D * 2;
   constexpr int BUF = 2 * TILE;  // K | V
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -271,8 +274,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(BwdP p) {
     int kind = TILE_EMPTY;
     if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
     if (kind == TILE_FULL && c0 + TL > p.Lkv) kind = TILE_PARTIAL;
+    kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {
+      const bool masked = kind == TILE_PARTIAL;
+      unsigned long long bits = ~0ull;
+      if (masked) bits = tile_bits(m, b, my_q, qok, c0, p.Lkv, true);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         f32x16 st = f32x16{}, dp = f32x16{};
@@ -283,11 +290,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(BwdP p) {
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float pv = __builtin_amdgcn_exp2f(st[r] * p.scale_log2 - L2);
-          if (kind == TILE_PARTIAL) {
-            const long key = c0 + 32 * kb + acc_row(r, h);
-            if (key >= p.Lkv || !qok || !allowed(m, b, my_fq, frame_of(m, key))) pv = 0.f;
-          }
+          float pv = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L2));
+          if (masked && !((bits >> (32 * kb + acc_row(r, h))) & 1ull)) pv = 0.f;
           dp[r] = pv * (dp[r] - Dl);
         }
 #pragma unroll

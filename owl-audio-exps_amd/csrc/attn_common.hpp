@@ -71,6 +71,24 @@ DEV bool allowed(const MaskP& m, long b, int fq, int fk) {
   return true;
 }
 
+// 64-bit allowed-mask of one lane against a 64-row tile of the other side: bit i set iff
+// (self, other0 + i) is allowed.  self_is_query selects which side `self` indexes.  Only built
+// for PARTIAL tiles, so the FULL-tile hot path carries no mask arithmetic at all.
+DEV unsigned long long tile_bits(const MaskP& m, long b, long self, bool self_ok, long other0, long other_len,
+                                 bool self_is_query) {
+  unsigned long long bits = 0ull;
+  if (!self_ok) return 0ull;
+  const int fs = frame_of(m, self + (self_is_query ? m.q_offset : 0));
+  for (int i = 0; i < 64; ++i) {
+    const long o = other0 + i;
+    if (o >= other_len) break;
+    const int fo = frame_of(m, o + (self_is_query ? 0 : m.q_offset));
+    const bool ok = self_is_query ? allowed(m, b, fs, fo) : allowed(m, b, fo, fs);
+    bits |= (unsigned long long)ok << i;
+  }
+  return bits;
+}
+
 // 128-B-row (64 x bf16) tile swizzles: K is read row-wise (ds_read_b128), V through
 // ds_read_b64_tr_b16; each gets its own conflict-free XOR of the 16-B chunk index.
 DEV int swz_row(int r) { return (r >> 1) & 7; }
@@ -136,6 +154,27 @@ DEV bf16x8 acc_frag(const f32x16& a, int s) {
 
 // row (register) index -> row of a 32x32 accumulator tile for lane half h
 DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// LDS-DMA (global_load_lds_dwordx4) of a 64 x 128-B tile by 4 waves: wave w moves rows
+// [16w, 16w + 16) in two 1-KiB wave-instructions.  The LDS image is lane-linear, so the chunk
+// swizzle is applied to the per-lane SOURCE chunk (an XOR is its own inverse).  Rows past R are
+// clamped to R - 1 (valid memory; the consumer masks them).
+template <int S>
+DEV void tile_glds(char* lds, const bf16* base, long ld, long r0, long R, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * wave + 8 * i + (lane >> 3);
+    const int ch = (lane & 7) ^ swz<S>(row);
+    long gr = r0 + row;
+    gr = gr < R ? gr : R - 1;
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(base + gr * ld + ch * 8),
+                                     (void __attribute__((address_space(3)))*)(lds + (16 * wave + 8 * i) * 128), 16,
+                                     0, 0);
+  }
+}
+
+#define OWLK_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#define OWLK_BARRIER() asm volatile("s_barrier" ::: "memory")
 
 MaskP owlk_make_mask(long tpf, int window, int causal, long q_offset, long Lkv, const int* kv_lo, const int* q_hi,
                      const int* run_start, const int* doc, long fstride);

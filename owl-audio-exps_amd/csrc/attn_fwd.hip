@@ -12,6 +12,9 @@
 // through ds_read_b64_tr_b16).  K/V tiles are register-staged into a double-buffered LDS ring.
 #include "attn_common.hpp"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace {
 
 constexpr int D = 64;
@@ -53,8 +56,12 @@ DEV void stage_store(char* lds, const bf16x8 (&r)[2]) {
   }
 }
 
+// GLDS = true: K/V tiles arrive by LDS-DMA into a 3-deep ring with two tiles in flight (no
+// staging registers, counted vmcnt + raw s_barrier); false: register-staged double buffer.
+template <bool GLDS>
 __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * KT * D * 2];  // [buf][K|V][64][64]
+  constexpr int NBUF = GLDS ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * KT * D * 2];  // [buf][K|V][64][64]
   __shared__ int red_lo;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, ql = lane & 31;
@@ -107,31 +114,58 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   o[1] = f32x16{};
   float mrow = -INFINITY, lrow = 0.f;
 
+  constexpr int BUFB = 2 * KT * D * 2;
   bf16x8 kr[2], vr[2];
-  if (ntiles > 0) {
-    stage_load(kr, K, p.ldk, kv_begin, p.Lkv);
-    stage_load(vr, V, p.ldv, kv_begin, p.Lkv);
-    stage_store<false>(smem, kr);
-    stage_store<true>(smem + KT * D * 2, vr);
+  if (GLDS) {
+    if (ntiles > 0) {
+      tile_glds<SW_ROW>(smem, K, p.ldk, kv_begin, p.Lkv, w, lane);
+      tile_glds<SW_TR>(smem + KT * D * 2, V, p.ldv, kv_begin, p.Lkv, w, lane);
+    }
+    if (ntiles > 1) {
+      tile_glds<SW_ROW>(smem + BUFB, K, p.ldk, kv_begin + KT, p.Lkv, w, lane);
+      tile_glds<SW_TR>(smem + BUFB + KT * D * 2, V, p.ldv, kv_begin + KT, p.Lkv, w, lane);
+      OWLK_VMCNT(4);
+    } else {
+      OWLK_VMCNT(0);
+    }
+    OWLK_BARRIER();
+  } else {
+    if (ntiles > 0) {
+      stage_load(kr, K, p.ldk, kv_begin, p.Lkv);
+      stage_load(vr, V, p.ldv, kv_begin, p.Lkv);
+      stage_store<false>(smem, kr);
+      stage_store<true>(smem + KT * D * 2, vr);
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const long c0 = kv_begin + (long)t * KT;
     const bool more = t + 1 < ntiles;
-    if (more) {
+    const bool more2 = t + 2 < ntiles;
+    if (GLDS) {
+      if (more2) {
+        char* nb = smem + ((t + 2) % 3) * BUFB;
+        tile_glds<SW_ROW>(nb, K, p.ldk, c0 + 2 * KT, p.Lkv, w, lane);
+        tile_glds<SW_TR>(nb + KT * D * 2, V, p.ldv, c0 + 2 * KT, p.Lkv, w, lane);
+      }
+    } else if (more) {
       stage_load(kr, K, p.ldk, c0 + KT, p.Lkv);
       stage_load(vr, V, p.ldv, c0 + KT, p.Lkv);
     }
-    const char* lk = smem + (t & 1) * (2 * KT * D * 2);
+    const char* lk = smem + (GLDS ? (t % 3) : (t & 1)) * BUFB;
     const char* lv = lk + KT * D * 2;
 
     const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
     int kind = TILE_EMPTY;
     if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
     if (kind == TILE_FULL && c0 + KT > p.Lkv) kind = TILE_PARTIAL;
+    kind = __builtin_amdgcn_readfirstlane(kind);  // wave-uniform: scalar branch, no exec masking
 
     if (kind != TILE_EMPTY) {
+      const bool masked = kind == TILE_PARTIAL;
+      unsigned long long bits = ~0ull;
+      if (masked) bits = tile_bits(m, b, my_q, my_q < p.Lq, c0, p.Lkv, true);
       // S^T[key][q] for two 32-key blocks
       f32x16 st[2];
 #pragma unroll
@@ -144,16 +178,13 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
           st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[kb], 0, 0, 0);
         }
       }
-      // mask, row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
+      // row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
       float tmax = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (kind == TILE_PARTIAL) {
-            const long key = c0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (key >= p.Lkv || my_q >= p.Lq || !allowed(m, b, my_fq, frame_of(m, key))) st[kb][r] = -INFINITY;
-          }
+          if (masked && !((bits >> (32 * kb + acc_row(r, h))) & 1ull)) st[kb][r] = -INFINITY;
           tmax = fmaxf(tmax, st[kb][r]);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
@@ -184,28 +215,27 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 pf;
+          const bf16x8 pf = acc_frag(st[kb], s);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) pf[j] = (bf16)st[kb][8 * s + j];
-          const int g = lane >> 4;
-          const int qq = (lane & 15) >> 2, pp = lane & 3;
-          const int rowa = 32 * kb + 16 * s + 4 * h + qq;
-          const int rowb = rowa + 8;
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            const int ch = 4 * db + 2 * (g & 1) + (pp >> 1);
-            const s16x4 lo = ds_read_tr16(lv + rowa * 128 + ((ch ^ swz_tr(rowa)) << 4) + 8 * (pp & 1));
-            const s16x4 hi = ds_read_tr16(lv + rowb * 128 + ((ch ^ swz_tr(rowb)) << 4) + 8 * (pp & 1));
-            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(join_tr(lo, hi), pf, o[db], 0, 0, 0);
-          }
+          for (int db = 0; db < 2; ++db)
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_TR>(lv, 32 * kb, s, db, lane), pf, o[db], 0, 0,
+                                                            0);
         }
     }
-    if (more) {
-      char* nb = smem + ((t + 1) & 1) * (2 * KT * D * 2);
-      stage_store<false>(nb, kr);
-      stage_store<true>(nb + KT * D * 2, vr);
+    if (GLDS) {
+      if (more2)
+        OWLK_VMCNT(4);  // tile t+1 landed (this wave's part); t+2 may stay in flight
+      else
+        OWLK_VMCNT(0);
+      OWLK_BARRIER();
+    } else {
+      if (more) {
+        char* nb = smem + ((t + 1) & 1) * BUFB;
+        stage_store<false>(nb, kr);
+        stage_store<true>(nb + KT * D * 2, vr);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 
   // ---- epilogue: O = O^T / l, lse
@@ -266,6 +296,10 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
   p.scale_log2 = scale * LOG2E;
   p.m = owlk_make_mask(tpf, window, causal, q_offset, Lkv, kv_lo, q_hi, run_start, doc, fstride);
   dim3 grid((unsigned)((Lq + QT - 1) / QT), (unsigned)H, (unsigned)B);
-  hipLaunchKernelGGL(attn_fwd_k, grid, dim3(256), 0, (hipStream_t)stream, p);
+  static const int variant = getenv("OWLK_ATTN_FWD_REGSTAGE") ? 0 : 1;
+  if (variant)
+    hipLaunchKernelGGL(attn_fwd_k<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(attn_fwd_k<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
   return owlk::check_launch("attn_fwd");
 }

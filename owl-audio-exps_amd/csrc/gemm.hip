@@ -14,6 +14,8 @@
 // through LDS so every global access is a 16-B row chunk.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace {
 
 enum Epi : int {
@@ -38,6 +40,7 @@ struct GemmP {
   const bf16* gate; long ldgate, sGate, tpf;
   const bf16* resid; long ldres, sRes;
   int tiles_m, tiles_n;
+  long kchunk;  // split-K: K range per blockIdx.y (multiple of BK); fp32 atomics combine the splits
 };
 
 // 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
@@ -114,6 +117,74 @@ DEV bf16x8 read_frag(const char* lds, int row0, int kk, int lane) {
   }
 }
 
+// epilogue for 8 consecutive outputs C[gm, gn .. gn + 8) of batch item z (v = raw accumulators)
+template <int EPI, bool OF32>
+DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
+  float bb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bb[e] = p.bias ? rb(p.bias[gn + e]) : 0.f;
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
+    if (OF32) {
+      float* C = (float*)p.C + z * p.sC + gm * p.ldc + gn;
+      if (p.beta != 0.f) {
+        const f32x4 o0 = *(const f32x4*)C, o1 = *(const f32x4*)(C + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += p.beta * o0[e];
+          v[e + 4] += p.beta * o1[e];
+        }
+      }
+      *(f32x4*)C = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      bf16* C = (bf16*)p.C + z * p.sC + gm * p.ldc + gn;
+      if (p.beta != 0.f) {
+        float o[8];
+        unpack8(*(const bf16x8*)C, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += p.beta * o[e];
+      }
+      *(bf16x8*)C = pack8(v);
+    }
+  } else if (EPI == EPI_SILU) {
+    float y[8], s[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      y[e] = rb(v[e] + bb[e]);
+      s[e] = silu_f(y[e]);
+    }
+    *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(s);
+  } else if (EPI == EPI_GATE_RESID) {
+    float y[8], g[8], r[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = rb(v[e] + bb[e]);
+    unpack8(*(const bf16x8*)(p.gate + z * p.sGate + (gm / p.tpf) * p.ldgate + gn), g);
+    unpack8(*(const bf16x8*)(p.resid + z * p.sRes + gm * p.ldres + gn), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = r[e] + rb(g[e] * y[e]);
+    if (p.aux) *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  } else if (EPI == EPI_DSILU) {
+    float x[8], o[8];
+    unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sg = 1.f / (1.f + __expf(-x[e]));
+      o[e] = rb(v[e]) * sg * (1.f + x[e] * (1.f - sg));
+    }
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  } else if (EPI == EPI_AXPBY) {
+    float x[8], o[8];
+    unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * x[e]));
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  }
+}
+
 template <int BM, int BN, bool AT, bool BT, int EPI, bool OF32>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;  // wave tile
@@ -149,9 +220,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)((p.K + BK - 1) / BK);
-  sa.load(A, p.lda, m0, 0, p.M, p.K);
-  sb.load(B, p.ldb, n0, 0, p.N, p.K);
+  const long kbeg = (long)blockIdx.y * p.kchunk;
+  const long kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
+  sa.load(A, p.lda, m0, kbeg, p.M, p.K);
+  sb.load(B, p.ldb, n0, kbeg, p.N, p.K);
   sa.store(smem);
   sb.store(smem + A_BYTES);
   __syncthreads();
@@ -160,8 +233,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      sa.load(A, p.lda, m0, (long)(kt + 1) * BK, p.M, p.K);
-      sb.load(B, p.ldb, n0, (long)(kt + 1) * BK, p.N, p.K);
+      sa.load(A, p.lda, m0, kbeg + (long)(kt + 1) * BK, p.M, p.K);
+      sb.load(B, p.ldb, n0, kbeg + (long)(kt + 1) * BK, p.N, p.K);
     }
     const char* la = smem + cur * (A_BYTES + B_BYTES);
     const char* lb = la + A_BYTES;
@@ -199,6 +272,21 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
     }
   __syncthreads();
 
+  if (OF32 && EPI == EPI_STORE && gridDim.y > 1) {
+    // split-K partial: each wave-instruction adds 64 consecutive floats (256 B, full atomic rate)
+    float* C = (float*)p.C + z * p.sC;
+    for (int row = wave; row < BM; row += NT / 64) {
+      const long gm = m0 + row;
+      if (gm >= p.M) break;
+#pragma unroll
+      for (int cc = 0; cc < BN; cc += 64) {
+        const long gn = n0 + cc + lane;
+        if (gn < p.N) atomicAdd(C + gm * p.ldc + gn, p.alpha * ct[row * EPI_LD + cc + lane]);
+      }
+    }
+    return;
+  }
+
   constexpr int CH = BM * BN / 8;
   for (int c = threadIdx.x; c < CH; c += NT) {
     const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
@@ -214,70 +302,148 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
         v[e + 4] = hi[e];
       }
     }
-    float bb[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bb[e] = p.bias ? rb(p.bias[gn + e]) : 0.f;
+    epi_chunk<EPI, OF32>(p, z, gm, gn, v);
+  }
+}
 
-    if (EPI == EPI_STORE) {
+
+// ======================================================================== 256 x 256 tiles
+// 8 waves (2 x 4, each 128 x 64), BK 64, operands moved by LDS-DMA (global_load_lds_dwordx4)
+// into a 2-stage ring: the next K-step's tiles stream in while the current one feeds 64 MFMAs
+// per wave.  Operand bytes per FLOP are half the 128x128 kernel's, which at peak needs more
+// L2 -> CU bandwidth (~64 B/clk/CU) than an XCD's L2 delivers.  The LDS-DMA image is lane-linear,
+// so the operand swizzles are applied to the per-lane source chunk (XOR: its own inverse).
+// Requirements (checked on the host): K % 64 == 0, tiled dims multiples of 256 for transposed
+// operands, rows of k-contiguous operands may have a ragged last tile (rows clamped).
+constexpr int NT8 = 512;
+
+template <int ROWS, bool TRANS>
+DEV void glds_tile(char* lds, const bf16* base, long ld, long r0, long k0, long R, int wave, int lane) {
+  if (!TRANS) {  // [ROWS][64] k-contiguous: 8 rows x 128 B per wave-instruction
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
-      if (OF32) {
-        float* C = (float*)p.C + z * p.sC + gm * p.ldc + gn;
-        if (p.beta != 0.f) {
-          const f32x4 o0 = *(const f32x4*)C, o1 = *(const f32x4*)(C + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] += p.beta * o0[e];
-            v[e + 4] += p.beta * o1[e];
-          }
-        }
-        *(f32x4*)C = f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else {
-        bf16* C = (bf16*)p.C + z * p.sC + gm * p.ldc + gn;
-        if (p.beta != 0.f) {
-          float o[8];
-          unpack8(*(const bf16x8*)C, o);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += p.beta * o[e];
-        }
-        *(bf16x8*)C = pack8(v);
-      }
-    } else if (EPI == EPI_SILU) {
-      float y[8], s[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        y[e] = rb(v[e] + bb[e]);
-        s[e] = silu_f(y[e]);
-      }
-      *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
-      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(s);
-    } else if (EPI == EPI_GATE_RESID) {
-      float y[8], g[8], r[8], o[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = rb(v[e] + bb[e]);
-      unpack8(*(const bf16x8*)(p.gate + z * p.sGate + (gm / p.tpf) * p.ldgate + gn), g);
-      unpack8(*(const bf16x8*)(p.resid + z * p.sRes + gm * p.ldres + gn), r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = r[e] + rb(g[e] * y[e]);
-      if (p.aux) *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
-      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
-    } else if (EPI == EPI_DSILU) {
-      float x[8], o[8];
-      unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float sg = 1.f / (1.f + __expf(-x[e]));
-        o[e] = rb(v[e]) * sg * (1.f + x[e] * (1.f - sg));
-      }
-      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
-    } else if (EPI == EPI_AXPBY) {
-      float x[8], o[8];
-      unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * x[e]));
-      *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    for (int i = 0; i < ROWS / 64; ++i) {
+      const int rbase = (wave * (ROWS / 64) + i) * 8;
+      const int row = rbase + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      long gr = r0 + row;
+      gr = gr < R ? gr : R - 1;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(base + gr * ld + k0 + ch * 8),
+                                       (void __attribute__((address_space(3)))*)(lds + rbase * 128), 16, 0, 0);
     }
+  } else {  // [64][ROWS] m/n-contiguous: 1 KiB = 1024 / (2 ROWS) k-rows per wave-instruction
+    constexpr int KPI = 512 / ROWS;  // k-rows per instruction
+    constexpr int CPR = ROWS / 8;    // 16-B chunks per k-row
+#pragma unroll
+    for (int i = 0; i < 64 / KPI / 8; ++i) {
+      const int kb = (wave * (64 / KPI / 8) + i) * KPI;
+      const int k = kb + lane / CPR;
+      const int pch = lane % CPR;
+      const int lch = ((((pch >> 1) ^ swz_t<ROWS>(k))) << 1) | (pch & 1);
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(base + (k0 + k) * ld + r0 + lch * 8),
+          (void __attribute__((address_space(3)))*)(lds + kb * ROWS * 2), 16, 0, 0);
+    }
+  }
+}
+
+template <bool AT, bool BT, int EPI, bool OF32>
+__global__ __launch_bounds__(NT8, 1) void gemm256_kernel(GemmP p) {
+  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64, TM = 8, TN = 4;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];  // 128 KiB
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+  const long z = blockIdx.z;
+  const bf16* A = p.A + z * p.sA;
+  const bf16* B = p.B + z * p.sB;
+  const long kbeg = (long)blockIdx.y * p.kchunk;
+  const long kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = (int)((kend - kbeg) / BK);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  glds_tile<BM, AT>(smem, A, p.lda, m0, kbeg, p.M, wave, lane);
+  glds_tile<BN, BT>(smem + A_BYTES, B, p.ldb, n0, kbeg, p.N, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      char* nb = smem + (cur ^ 1) * STAGE;
+      glds_tile<BM, AT>(nb, A, p.lda, m0, kbeg + (long)(kt + 1) * BK, p.M, wave, lane);
+      glds_tile<BN, BT>(nb + A_BYTES, B, p.ldb, n0, kbeg + (long)(kt + 1) * BK, p.N, wave, lane);
+    }
+    const char* la = smem + cur * STAGE;
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<BN, BT>(lb, wn * WTN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = read_frag<BM, AT>(la, wm * WTM + 16 * i, kk, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue per wave through a private 16 x 64 fp32 LDS strip (reuses the staging ring)
+  float* strip = (float*)smem + wave * (16 * 68);
+  const bool atomic = OF32 && EPI == EPI_STORE && gridDim.y > 1;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * 68 + 16 * j + (lane & 15)] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const long rbase = m0 + wm * WTM + 16 * i;
+    if (atomic) {
+      float* C = (float*)p.C + z * p.sC;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const long gm = rbase + rr;
+        if (gm < p.M) atomicAdd(C + gm * p.ldc + n0 + wn * WTN + lane, p.alpha * strip[rr * 68 + lane]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = lane + 64 * q;
+        const int rr = c >> 3, col = (c & 7) * 8;
+        const long gm = rbase + rr, gn = n0 + wn * WTN + col;
+        float v[8];
+        const f32x4 lo = *(const f32x4*)(strip + rr * 68 + col);
+        const f32x4 hi = *(const f32x4*)(strip + rr * 68 + col + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lo[e];
+          v[e + 4] = hi[e];
+        }
+        if (gm < p.M) epi_chunk<EPI, OF32>(p, z, gm, gn, v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
 
@@ -285,7 +451,8 @@ template <int BM, int BN, bool AT, bool BT, int EPI, bool OF32>
 int launch(GemmP& p, long batch, hipStream_t s) {
   p.tiles_m = (int)((p.M + BM - 1) / BM);
   p.tiles_n = (int)((p.N + BN - 1) / BN);
-  dim3 grid(p.tiles_m * p.tiles_n, 1, (unsigned)batch);
+  const int splits = (int)((p.K + p.kchunk - 1) / p.kchunk);
+  dim3 grid(p.tiles_m * p.tiles_n, (unsigned)splits, (unsigned)batch);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, AT, BT, EPI, OF32>), grid, dim3(NT), 0, s, p);
   return owlk::check_launch("gemm");
 }
@@ -313,6 +480,38 @@ int dispatch_e(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStrea
   return 1;
 }
 
+
+template <bool AT, bool BT, int EPI, bool OF32>
+int launch256(GemmP& p, long batch, hipStream_t s) {
+  p.tiles_m = (int)((p.M + 255) / 256);
+  p.tiles_n = (int)((p.N + 255) / 256);
+  const int splits = (int)((p.K + p.kchunk - 1) / p.kchunk);
+  dim3 grid(p.tiles_m * p.tiles_n, (unsigned)splits, (unsigned)batch);
+  hipLaunchKernelGGL((gemm256_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  return owlk::check_launch("gemm256");
+}
+
+template <int EPI, bool OF32>
+int dispatch256_t(GemmP& p, int at, int bt, long batch, hipStream_t s) {
+  if (!at && !bt) return launch256<false, false, EPI, OF32>(p, batch, s);
+  if (!at && bt) return launch256<false, true, EPI, OF32>(p, batch, s);
+  if (at && bt) return launch256<true, true, EPI, OF32>(p, batch, s);
+  return launch256<true, false, EPI, OF32>(p, batch, s);
+}
+
+int dispatch256(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE:
+      return cf32 ? dispatch256_t<EPI_STORE, true>(p, at, bt, batch, s)
+                  : dispatch256_t<EPI_STORE, false>(p, at, bt, batch, s);
+    case EPI_SILU: return dispatch256_t<EPI_SILU, false>(p, at, bt, batch, s);
+    case EPI_GATE_RESID: return dispatch256_t<EPI_GATE_RESID, false>(p, at, bt, batch, s);
+    case EPI_DSILU: return dispatch256_t<EPI_DSILU, false>(p, at, bt, batch, s);
+    case EPI_AXPBY: return dispatch256_t<EPI_AXPBY, false>(p, at, bt, batch, s);
+  }
+  owlk::set_error("gemm: unknown epilogue %d", epi);
+  return 1;
+}
 }  // namespace
 
 extern "C" int owlk_gemm(long M, long N, long K, long batch,
@@ -343,8 +542,34 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   p.gate = (const bf16*)gate; p.ldgate = ldgate; p.sGate = sGate; p.tpf = tpf > 0 ? tpf : 1;
   p.resid = (const bf16*)resid; p.ldres = ldres; p.sRes = sRes;
   hipStream_t s = (hipStream_t)stream;
-  // small outputs (per-frame modulation, Newton-Schulz) use 64x64 tiles to fill the chip
   const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
+  const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
+  p.kchunk = K;
+  static const int use256 = getenv("OWLK_GEMM_NO256") ? 0 : 1;
+  const bool fits256 = use256 && K % 64 == 0 && N % 256 == 0 && (!a_trans || M % 256 == 0) &&
+                       (!b_trans || N % 256 == 0) && !(c_f32 && beta != 0.f && beta != 1.f);
+  if (fits256) {
+    if (c_f32 && epi == EPI_STORE && beta == 1.f && K >= 8192 && tiles256 < 1024) {
+      long splits = (512 + tiles256 - 1) / tiles256;
+      if (splits > K / 4096) splits = K / 4096;
+      if (splits > 1) {
+        p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+        return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
+      }
+    }
+    if (tiles256 >= 256) return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
+  }
+  // long reductions onto small outputs (weight gradients, K = tokens): 128x128 tiles, K split so
+  // the grid covers ~4 workgroups per CU; the fp32 output must be zeroed by the caller (beta = 1)
+  if (c_f32 && epi == EPI_STORE && beta == 1.f && K >= 8192 && tiles128 < 1024) {
+    long splits = (1024 + tiles128 - 1) / tiles128;
+    if (splits > K / 4096) splits = K / 4096;
+    if (splits > 1) {
+      p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+      return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
+    }
+  }
+  // small outputs (per-frame modulation, Newton-Schulz) use 64x64 tiles to fill the chip
   if (tiles128 < 512) return dispatch_e<64, 64>(p, a_trans, b_trans, epi, c_f32, batch, s);
   return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
 }

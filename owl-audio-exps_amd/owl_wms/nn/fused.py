@@ -74,7 +74,7 @@ class LinearFn(torch.autograd.Function):
                 dx = dx[:, : ctx.shp[-1]]
             dx = dx.reshape(ctx.shp).to(ctx.xdtype)
         if ctx.needs_input_grad[1]:
-            dw = K.gemm(dy2, x2, a_trans=True, b_trans=True, out_f32=True)
+            dw = K.gemm_wgrad(dy2, x2)
             if ctx.pad:
                 dw = dw[:, : ctx.shp[-1]].contiguous()
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -170,9 +170,9 @@ class DiTBlockFn(torch.autograd.Function):
         dy2, dg2, dbf2 = K.gate_bwd(dx2, y2, gg2, tpf)
         db2 = dbf2.sum(0)
         dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre)
-        dw2 = K.gemm(dy2, a, a_trans=True, b_trans=True, out_f32=True)
+        dw2 = K.gemm_wgrad(dy2, a)
         db1 = K.colsum(dapre)
-        dw1 = K.gemm(dapre, h2, a_trans=True, b_trans=True, out_f32=True)
+        dw1 = K.gemm_wgrad(dapre, h2)
         dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
         del dapre
         dx1, dmod2 = K.adaln_bwd(dh2, x1, r2, a2[:, :d], tpf, dres=dx2)
@@ -182,7 +182,7 @@ class DiTBlockFn(torch.autograd.Function):
         dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf)
         dbout = dbf1.sum(0)
         do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
-        dwout = K.gemm(dy1, o, a_trans=True, b_trans=True, out_f32=True)
+        dwout = K.gemm_wgrad(dy1, o)
         del dy1
         dqkv = torch.empty(M, 3 * d, device=xx.device, dtype=BF16)
         dqkr = torch.empty(M, 2 * d, device=xx.device, dtype=BF16)
@@ -194,7 +194,7 @@ class DiTBlockFn(torch.autograd.Function):
         K.qk_rope_bwd(dqkr, qkv, rq, H, D, geo.cos, geo.sin, dqkv, geo.tab_off, T)
         del dqkr
         dbqkv = K.colsum(dqkv)
-        dwqkv = K.gemm(dqkv, h1, a_trans=True, b_trans=True, out_f32=True)
+        dwqkv = K.gemm_wgrad(dqkv, h1)
         dh1 = K.gemm(dqkv, bf16_weight(wqkv), b_trans=True)
         del dqkv
         dx, dmod1 = K.adaln_bwd(dh1, xx, r1, a1[:, :d], tpf, dres=dx1)

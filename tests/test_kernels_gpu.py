@@ -241,3 +241,12 @@ def test_newton_schulz_matches_oracle(shape):
     assert rel(y, ref) < 4e-2
     sv, sr = torch.linalg.svdvals(y), torch.linalg.svdvals(ref)
     assert (sv - sr).abs().max() < 0.05
+
+
+@pytest.mark.parametrize("M,N,K_", [(128, 1536, 16384), (1536, 1536, 20480), (4608, 256, 12288)])
+def test_gemm_splitk_weight_grad(M, N, K_):
+    k = K()
+    dy, x = rnd(K_, M, seed=70), rnd(K_, N, seed=71)
+    ref = dy.float().T @ x.float()
+    out = k.gemm_wgrad(dy, x)
+    assert rel(out, ref) < 1e-5

@@ -1,0 +1,59 @@
+"""Time libowlk GEMMs at the dit_v4 shapes (M = 98,304 tokens) beside torch.matmul (hipBLASLt).
+
+    python tools/gemm_bench.py
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "owl-audio-exps_amd")]
+import torch  # noqa: E402
+
+from owl_wms import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    T, d = 98304, 1536
+    torch.manual_seed(0)
+    r = lambda *s: (torch.randn(*s, device="cuda") * 0.5).to(torch.bfloat16)
+    cases = [  # (name, A, B, a_trans, b_trans, M, N, K)
+        ("qkv fwd", r(T, d), r(3 * d, d), False, False),
+        ("fc1 fwd", r(T, d), r(4 * d, d), False, False),
+        ("fc2 fwd", r(T, 4 * d), r(d, 4 * d), False, False),
+        ("out fwd", r(T, d), r(d, d), False, False),
+        ("fc2 dX", r(T, d), r(d, 4 * d), False, True),
+        ("qkv dX", r(T, 3 * d), r(3 * d, d), False, True),
+        ("fc1 dW", r(T, 4 * d), r(T, d), True, True),
+        ("qkv dW", r(T, 3 * d), r(T, d), True, True),
+        ("out dW", r(T, d), r(T, d), True, True),
+    ]
+    for name, A, B, at, bt in cases:
+        M = A.shape[1] if at else A.shape[0]
+        N = B.shape[1] if bt else B.shape[0]
+        Kd = A.shape[0] if at else A.shape[1]
+        fl = 2.0 * M * N * Kd
+        if at:
+            ours = timeit(lambda: K.gemm_wgrad(A, B))
+        else:
+            ours = timeit(lambda: K.gemm(A, B, b_trans=bt))
+        Am = A.T if at else A
+        Bm = B if bt else B.T
+        ref = timeit(lambda: torch.matmul(Am, Bm))
+        print(f"{name:8s} [{M}x{N}x{Kd}]  owlk {ours:7.3f} ms {fl / ours / 1e9:7.1f} TF/s | "
+              f"hipBLASLt {ref:7.3f} ms {fl / ref / 1e9:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
