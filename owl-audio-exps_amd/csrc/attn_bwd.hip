@@ -148,8 +148,8 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
-      unsigned long long bits = ~0ull;
-      if (masked) bits = tile_bits(m, b, my_k, my_k < p.Lkv, q0, p.Lq, false);
+      unsigned long long bh = 0ull;
+      if (masked) bh = tile_bits(m, b, my_k, my_k < p.Lkv, q0, p.Lq, false) >> (4 * h);
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         f32x16 st = f32x16{}, dp = f32x16{};
@@ -166,12 +166,18 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g4 + e;
-            float pv = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L[e]));
-            if (masked && !((bits >> (rowb + e)) & 1ull)) pv = 0.f;
-            st[r] = pv;
-            dp[r] = pv * (dp[r] - Dl[e]);
+            st[r] = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L[e]));
+            dp[r] -= Dl[e];
           }
         }
+        if (masked) {
+          if (qb == 0)
+            apply_bits<0>(st, bh, 0.f);
+          else
+            apply_bits<32>(st, bh, 0.f);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[r] *= st[r];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const bf16x8 pf = acc_frag(st, s), sf = acc_frag(dp, s);
@@ -278,8 +284,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
 
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
-      unsigned long long bits = ~0ull;
-      if (masked) bits = tile_bits(m, b, my_q, qok, c0, p.Lkv, true);
+      unsigned long long bh = 0ull;
+      if (masked) bh = tile_bits(m, b, my_q, qok, c0, p.Lkv, true) >> (4 * h);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         f32x16 st = f32x16{}, dp = f32x16{};
@@ -289,11 +295,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_ROW>(lv, 32 * kb, s, lane), df[s], dp, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float pv = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L2));
-          if (masked && !((bits >> (32 * kb + acc_row(r, h))) & 1ull)) pv = 0.f;
-          dp[r] = pv * (dp[r] - Dl);
+        for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L2));
+        if (masked) {
+          if (kb == 0)
+            apply_bits<0>(st, bh, 0.f);
+          else
+            apply_bits<32>(st, bh, 0.f);
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[r] = st[r] * (dp[r] - Dl);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const bf16x8 sf = acc_frag(dp, s);

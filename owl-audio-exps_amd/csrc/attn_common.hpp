@@ -89,6 +89,18 @@ DEV unsigned long long tile_bits(const MaskP& m, long b, long self, bool self_ok
   return bits;
 }
 
+// Replace the elements of a 32x32 accumulator block whose bit is clear by `fill`.  `bh` is the
+// tile mask shifted right by 4*h (h = lane >> 5), so element r of block BASE (0 or 32) is bit
+// BASE + (r & 3) + 8 * (r >> 2) -- a compile-time index.  Callers branch on a wave-uniform
+// "tile is PARTIAL" flag around this, so FULL tiles never execute it.
+template <int BASE>
+DEV void apply_bits(f32x16& a, unsigned long long bh, float fill) {
+  __asm__ volatile("");  // keeps the caller's uniform branch a branch (no if-conversion to selects)
+  const unsigned w = BASE ? (unsigned)(bh >> 32) : (unsigned)bh;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a[r] = (w >> ((r & 3) + 8 * (r >> 2))) & 1u ? a[r] : fill;
+}
+
 // 128-B-row (64 x bf16) tile swizzles: K is read row-wise (ds_read_b128), V through
 // ds_read_b64_tr_b16; each gets its own conflict-free XOR of the 16-B chunk index.
 DEV int swz_row(int r) { return (r >> 1) & 7; }

@@ -164,8 +164,6 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
 
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
-      unsigned long long bits = ~0ull;
-      if (masked) bits = tile_bits(m, b, my_q, my_q < p.Lq, c0, p.Lkv, true);
       // S^T[key][q] for two 32-key blocks
       f32x16 st[2];
 #pragma unroll
@@ -178,13 +176,17 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
           st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[kb], 0, 0, 0);
         }
       }
+      if (masked) {  // wave-uniform: only tiles straddling a mask edge
+        const unsigned long long bh = tile_bits(m, b, my_q, my_q < p.Lq, c0, p.Lkv, true) >> (4 * h);
+        apply_bits<0>(st[0], bh, -INFINITY);
+        apply_bits<32>(st[1], bh, -INFINITY);
+      }
       // row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
       float tmax = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (masked && !((bits >> (32 * kb + acc_row(r, h))) & 1ull)) st[kb][r] = -INFINITY;
           tmax = fmaxf(tmax, st[kb][r]);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
