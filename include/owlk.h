@@ -72,10 +72,14 @@ int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long 
  *   token / tpf for keys; causal; |fq - fk| < window (window <= 0: unlimited); doc[b, fq] ==
  *   doc[b, fk].  Frame helper arrays (int32 [B, n_frames], batch stride fstride, may be NULL
  *   without docs): kv_lo (first visible kv frame), q_hi (last query frame seeing a kv frame),
- *   run_start (first frame of the contiguous same-doc run). */
+ *   run_start (first frame of the contiguous same-doc run).
+ * score_bound: 0, or a bound on |q.k| the caller guarantees for every pair (QK-RMSNorm'd q, k:
+ *   sqrt(D) * sqrt(D) = D, attn.py:84, times 1 + a few bf16 ulps); the softmax then uses that
+ *   fixed offset instead of a running row max (same result, no per-tile max/rescale). */
 int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
                   long ldv, long svb, void* o, long ldo, long sob, float* lse, long B, int H, long Lq,
-                  long Lkv, int head_dim, float scale, long tpf, int window, int causal, long q_offset,
+                  long Lkv, int head_dim, float scale, float score_bound, long tpf, int window, int causal,
+                  long q_offset,
                   const int* kv_lo, const int* q_hi, const int* run_start, const int* doc, long fstride,
                   void* stream);
 /* delta[b, h, t] = sum_d dO * O (fp32), the backward's row constant */

@@ -32,6 +32,7 @@ struct FwdP {
   long Lq, Lkv;
   int H;
   float scale_log2;     // softmax scale * log2(e)
+  float bound;          // BOUNDED: |q.k| <= bound for every pair (raw score units)
   MaskP m;
 };
 
@@ -58,7 +59,12 @@ DEV void stage_store(char* lds, const bf16x8 (&r)[2]) {
 
 // GLDS = true: K/V tiles arrive by LDS-DMA into a 3-deep ring with two tiles in flight (no
 // staging registers, counted vmcnt + raw s_barrier); false: register-staged double buffer.
-template <bool GLDS>
+// BOUNDED = true: the caller guarantees |q.k| <= p.bound (QK-RMSNorm'd q, k have |q| = |k| =
+// sqrt(D), attn.py:84), so softmax uses the fixed offset m = bound: p = exp2((s - bound) c) is
+// in (0, 1] without a running max, and the online max / rescale work disappears from every tile.
+// Softmax is shift-invariant, so the result is the same function; P keeps bf16's relative
+// precision at any magnitude (exponent range of f32).
+template <bool GLDS, bool BOUNDED>
 __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   constexpr int NBUF = GLDS ? 3 : 2;
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * KT * D * 2];  // [buf][K|V][64][64]
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   f32x16 o[2];
   o[0] = f32x16{};
   o[1] = f32x16{};
-  float mrow = -INFINITY, lrow = 0.f;
+  float mrow = BOUNDED ? p.bound : -INFINITY, lrow = 0.f;
 
   constexpr int BUFB = 2 * KT * D * 2;
   bf16x8 kr[2], vr[2];
@@ -181,26 +187,29 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
         apply_bits<0>(st[0], bh, -INFINITY);
         apply_bits<32>(st[1], bh, -INFINITY);
       }
-      // row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
-      float tmax = -INFINITY;
+      float mc;
+      if constexpr (BOUNDED) {
+        mc = mrow * p.scale_log2;
+      } else {
+        // row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
+        float tmax = -INFINITY;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          tmax = fmaxf(tmax, st[kb][r]);
+          for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[kb][r]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mnew = fmaxf(mrow, tmax);
+        mc = mnew == -INFINITY ? 0.f : mnew * p.scale_log2;
+        if (__any(mnew > mrow)) {  // some row's max moved: rescale l and O (exactly)
+          const float alpha = __builtin_amdgcn_exp2f(mrow * p.scale_log2 - mc);
+          lrow *= alpha;
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(mrow, tmax);
-      const float mc = mnew == -INFINITY ? 0.f : mnew * p.scale_log2;
-      if (__any(mnew > mrow)) {  // some row's max moved: rescale l and O (exactly)
-        const float alpha = __builtin_amdgcn_exp2f(mrow * p.scale_log2 - mc);
-        lrow *= alpha;
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+        mrow = mnew;
       }
-      mrow = mnew;
       float psum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -280,9 +289,9 @@ MaskP owlk_make_mask(long tpf, int window, int causal, long q_offset, long Lkv, 
 
 extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
                              long ldv, long svb, void* o, long ldo, long sob, float* lse, long B, int H, long Lq,
-                             long Lkv, int head_dim, float scale, long tpf, int window, int causal, long q_offset,
-                             const int* kv_lo, const int* q_hi, const int* run_start, const int* doc, long fstride,
-                             void* stream) {
+                             long Lkv, int head_dim, float scale, float score_bound, long tpf, int window,
+                             int causal, long q_offset, const int* kv_lo, const int* q_hi, const int* run_start,
+                             const int* doc, long fstride, void* stream) {
   OWLK_REQUIRE(head_dim == D, "attn_fwd: head_dim %d not built (64 only)", head_dim);
   OWLK_REQUIRE(tpf > 0 && Lq > 0 && Lkv > 0 && B > 0 && H > 0, "attn_fwd: bad sizes");
   OWLK_REQUIRE((Lkv + q_offset) < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_fwd: sequence too long");
@@ -296,12 +305,19 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
   p.sqb = sqb; p.skb = skb; p.svb = svb; p.sob = sob;
   p.Lq = Lq; p.Lkv = Lkv; p.H = H;
   p.scale_log2 = scale * LOG2E;
+  p.bound = score_bound;
+  OWLK_REQUIRE(score_bound >= 0.f && score_bound * scale < 64.f, "attn_fwd: score_bound out of range");
   p.m = owlk_make_mask(tpf, window, causal, q_offset, Lkv, kv_lo, q_hi, run_start, doc, fstride);
   dim3 grid((unsigned)((Lq + QT - 1) / QT), (unsigned)H, (unsigned)B);
   static const int variant = getenv("OWLK_ATTN_FWD_REGSTAGE") ? 0 : 1;
-  if (variant)
-    hipLaunchKernelGGL(attn_fwd_k<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
+  const bool bounded = score_bound > 0.f;
+  if (variant && bounded)
+    hipLaunchKernelGGL((attn_fwd_k<true, true>), grid, dim3(256), 0, (hipStream_t)stream, p);
+  else if (variant)
+    hipLaunchKernelGGL((attn_fwd_k<true, false>), grid, dim3(256), 0, (hipStream_t)stream, p);
+  else if (bounded)
+    hipLaunchKernelGGL((attn_fwd_k<false, true>), grid, dim3(256), 0, (hipStream_t)stream, p);
   else
-    hipLaunchKernelGGL(attn_fwd_k<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL((attn_fwd_k<false, false>), grid, dim3(256), 0, (hipStream_t)stream, p);
   return owlk::check_launch("attn_fwd");
 }

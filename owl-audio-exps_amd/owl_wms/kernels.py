@@ -3,6 +3,8 @@
 Every function checks shapes/strides on the host before the launch (a kernel never sees an
 operand its grid does not cover) and enqueues on torch's current HIP stream.
 """
+import os
+
 import torch
 
 from ._lib import call, ptr, stream
@@ -183,9 +185,16 @@ def _v3(t, name):
     return t
 
 
-def attn_fwd(q, k, v, H, D, mask, scale=None, o=None):
+# |q.k| bound for QK-RMSNorm'd q, k (attn.py:84): |q| = |k| = sqrt(D) up to bf16 rounding of the
+# normalised, rotated values (<= 2^-8 relative each); 2 % margin.
+def qk_norm_bound(D):
+    return 0.0 if os.environ.get("OWLK_NO_SCORE_BOUND") else 1.02 * D
+
+
+def attn_fwd(q, k, v, H, D, mask, scale=None, o=None, score_bound=0.0):
     """Frame-masked flash attention.  q [B, Lq, >=H*D], k/v [B, Lkv, >=H*D] token-major views
-    (head h at columns h*D); returns o [B, Lq, H*D] bf16 and lse [B, H, Lq] fp32."""
+    (head h at columns h*D); returns o [B, Lq, H*D] bf16 and lse [B, H, Lq] fp32.
+    score_bound > 0 promises |q.k| <= score_bound (see qk_norm_bound): fixed-offset softmax."""
     _v3(q, "q"), _v3(k, "k"), _v3(v, "v")
     B, Lq, Lkv = q.shape[0], q.shape[1], k.shape[1]
     assert k.shape[0] == B and v.shape[:2] == k.shape[:2]
@@ -196,8 +205,8 @@ def attn_fwd(q, k, v, H, D, mask, scale=None, o=None):
     lse = torch.empty(B, H, Lq, device=q.device, dtype=F32)
     call("owlk_attn_fwd", ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
          ptr(v), v.stride(1), v.stride(0), ptr(o), o.stride(1), o.stride(0), ptr(lse), B, H, Lq, Lkv, D,
-         float(scale), mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), mask.q_offset,
-         *mask.args()[3:], stream(), key=f"attn_fwd[w{mask.window}]", flops=lambda: 4.0 * D * H * B * mask_pairs(mask, Lq, Lkv))
+         float(scale), float(score_bound), mask.tpf, 0 if mask.window is None else int(mask.window),
+         int(mask.causal), mask.q_offset, *mask.args()[3:], stream(), key=f"attn_fwd[w{mask.window}]", flops=lambda: 4.0 * D * H * B * mask_pairs(mask, Lq, Lkv))
     return o, lse
 
 

@@ -84,7 +84,7 @@ class Attn(nn.Module):
             mask = K.FrameMask(1, None, False, 0, None)
         else:
             mask = block_mask
-        o, _ = K.attn_fwd(q, k, v, H, D, mask)
+        o, _ = K.attn_fwd(q, k, v, H, D, mask, score_bound=K.qk_norm_bound(D))  # q, k RMS-normalised
         return o
 
 

@@ -141,7 +141,8 @@ class DiTBlockFn(torch.autograd.Function):
         qkv = K.gemm(h1, bf16_weight(wqkv), bias=bqkv)
         qkr, rq = K.qk_rope_fwd(qkv, H, D, geo.cos, geo.sin, geo.tab_off, T)
         q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
-        o, lse = K.attn_fwd(q3, k3, qkv.view(B, T, 3 * d)[:, :, 2 * d:], H, D, geo.mask)
+        o, lse = K.attn_fwd(q3, k3, qkv.view(B, T, 3 * d)[:, :, 2 * d:], H, D, geo.mask,
+                            score_bound=K.qk_norm_bound(D))
         o = o.view(M, d)
         y1 = torch.empty(M, d, device=x.device, dtype=BF16)
         x1 = K.gemm(o, bf16_weight(wout), bias=bout, epi=K.EPI_GATE_RESID, aux=y1, gate=gg1, tpf=tpf, resid=xx)

@@ -185,6 +185,30 @@ def test_attention_fwd_bwd(case):
         assert rel(got.view(B, L, H, D).transpose(1, 2), ref) < 2e-2
 
 
+@pytest.mark.parametrize("case", [ATTN_CASES[0], ATTN_CASES[2], ATTN_CASES[4], ATTN_CASES[6]])
+def test_attention_fwd_score_bound(case):
+    """Fixed-offset softmax (score_bound) on QK-RMSNorm'd inputs == oracle, and its lse equals
+    the running-max kernel's (softmax is shift invariant; only rounding differs)."""
+    k = K()
+    B, H, nf, tpf, window, docs = case
+    L, D = nf * tpf, 64
+    unit = lambda t: (t.float().view(-1, H, D) * torch.rsqrt(t.float().view(-1, H, D).pow(2).mean(-1, keepdim=True))
+                      ).bfloat16().view(B, L, H * D)
+    q, kk = unit(rnd(B * L, H * D, seed=60)), unit(rnd(B * L, H * D, seed=61))
+    v = rnd(B * L, H * D, seed=62).view(B, L, H * D)
+    doc = torch.zeros(B, nf, dtype=torch.long)
+    if docs:
+        doc[:, nf // 3:] = 1
+    mask = k.FrameMask(tpf, window, True, 0, k.frame_arrays(doc.to(DEV), nf, window) if docs else None)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask, score_bound=k.qk_norm_bound(D))
+    o0, lse0 = k.attn_fwd(q, kk, v, H, D, mask)
+    ref = R.attention(*(t.cpu().float().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v)),
+                      R.frame_mask(L, L, tpf, window, doc if docs else None))
+    assert rel(o.view(B, L, H, D).transpose(1, 2), ref) < 1e-2
+    assert (lse - lse0).abs().max().item() < 1e-4
+    assert rel(o, o0) < 5e-3
+
+
 def test_attention_dit_v4_shape_smoke():
     """Full dit_v4 attention shape (24 heads x 98,304 tokens): finite, rows normalised."""
     k = K()

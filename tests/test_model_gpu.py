@@ -1,7 +1,8 @@
 """Model-level parity of the HIP path against the reference's own golden vectors.
 
 Tolerances (bf16 autocast semantics on both sides):
-  |d loss| / loss <= 5e-3, prediction rel-L2 <= 2e-2, parameter-gradient rel-L2 <= 5e-2,
+  |d loss| / loss <= 5e-3, prediction rel-L2 <= 2e-2, parameter-gradient rel-L2 <= 2e-2 (bf16 inputs;
+  measured <= 5e-3) and grad norms within 5e-2 (both modes),
   config-1 10-step loss trajectory within 2e-2 relative per step (GPU bf16 vs reference fp32).
 """
 from types import SimpleNamespace
@@ -61,16 +62,16 @@ def test_gamerft_loss_pred_grads_vs_reference(mode):
     assert rel(d["pred_video"], GR[p + "pred"]) < 2e-2
     n_full = 0
     for i, (k, prm) in enumerate(sorted(m.named_parameters())):
-        # vs the fp32 reference, grads that are token sums of tiny cancelling products (per-frame
-        # modulation fcs, biases) differ under bf16 autocast in the reference itself -> bf16 only
-        if mode == "fp32" and ("adaln" in k or "gate" in k or "norm.fc" in k or k.endswith("bias")):
-            continue
         st = GR[p + "gradstat." + k]
         assert abs(prm.grad.double().norm().item() - st[3].item()) <= 5e-2 * st[3].item() + 1e-7, k
-        if p + "grad." + k in GR:
-            assert rel(prm.grad, GR[p + "grad." + k]) < 5e-2, k
+        # elementwise grads only vs the bf16-input reference: this path takes latents and ts in
+        # bf16 on entry (the reference trainer's bf16 loader under autocast, rft_trainer.py:146,
+        # 183-187); with fp32 inputs the reference keeps ts in fp32 and sin(1000 t) differs in
+        # phase, which moves cancellation-heavy grads by 15-30 % (loss, pred and norms still agree)
+        if mode == "bf16" and p + "grad." + k in GR:
+            assert rel(prm.grad, GR[p + "grad." + k]) < 2e-2, k
             n_full += 1
-    assert n_full >= 6
+    assert n_full >= 6 or mode == "fp32"
 
 
 def test_muon_step_on_reference_grads_gpu():
