@@ -74,8 +74,9 @@ int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long 
  *   without docs): kv_lo (first visible kv frame), q_hi (last query frame seeing a kv frame),
  *   run_start (first frame of the contiguous same-doc run).
  * score_bound: 0, or a bound on |q.k| the caller guarantees for every pair (QK-RMSNorm'd q, k:
- *   sqrt(D) * sqrt(D) = D, attn.py:84, times 1 + a few bf16 ulps); the softmax then uses that
- *   fixed offset instead of a running row max (same result, no per-tile max/rescale). */
+ *   sqrt(D) * sqrt(D) = D, attn.py:84, times 1 + a few bf16 ulps; scale * bound < 40); the
+ *   softmax then needs no running row max: p = exp2(c s) directly (same result, no per-tile
+ *   max / rescale; q is prescaled by c = scale * log2 e inside the kernel). */
 int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
                   long ldv, long svb, void* o, long ldo, long sob, float* lse, long B, int H, long Lq,
                   long Lkv, int head_dim, float scale, float score_bound, long tpf, int window, int causal,

@@ -185,6 +185,31 @@ DEV void tile_glds(char* lds, const bf16* base, long ld, long r0, long R, int wa
   }
 }
 
+// Same transfer with per-lane byte offsets precomputed once (they do not depend on the tile) and
+// a wave-uniform tile base, so each tile costs no VALU address arithmetic (saddr + voffset form).
+// Only for tiles fully inside the tensor (the caller keeps tile_glds for the ragged last tile).
+struct GldsOff {
+  unsigned o[2];
+};
+template <int S>
+DEV GldsOff glds_offsets(long ld, int wave, int lane) {
+  GldsOff g;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * wave + 8 * i + (lane >> 3);
+    const int ch = (lane & 7) ^ swz<S>(row);
+    g.o[i] = (unsigned)((row * ld + ch * 8) * 2);
+  }
+  return g;
+}
+DEV void tile_glds_fast(char* lds, const bf16* tile_base, const GldsOff& g, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)((const char*)tile_base + g.o[i]),
+                                     (void __attribute__((address_space(3)))*)(lds + (16 * wave + 8 * i) * 128), 16,
+                                     0, 0);
+}
+
 #define OWLK_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #define OWLK_BARRIER() asm volatile("s_barrier" ::: "memory")
 

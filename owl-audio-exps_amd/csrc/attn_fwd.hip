@@ -60,10 +60,9 @@ DEV void stage_store(char* lds, const bf16x8 (&r)[2]) {
 // GLDS = true: K/V tiles arrive by LDS-DMA into a 3-deep ring with two tiles in flight (no
 // staging registers, counted vmcnt + raw s_barrier); false: register-staged double buffer.
 // BOUNDED = true: the caller guarantees |q.k| <= p.bound (QK-RMSNorm'd q, k have |q| = |k| =
-// sqrt(D), attn.py:84), so softmax uses the fixed offset m = bound: p = exp2((s - bound) c) is
-// in (0, 1] without a running max, and the online max / rescale work disappears from every tile.
-// Softmax is shift-invariant, so the result is the same function; P keeps bf16's relative
-// precision at any magnitude (exponent range of f32).
+// sqrt(D), attn.py:84), so every exp2 argument c*s lies in [-c*bound, c*bound] (+-11.8 at D 64):
+// p = exp2(c s) needs no running max, no offset and no rescale.  Softmax is shift-invariant, so
+// the result is the same function; P keeps bf16's relative precision at any magnitude.
 template <bool GLDS, bool BOUNDED>
 __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   constexpr int NBUF = GLDS ? 3 : 2;
@@ -110,6 +109,19 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
 #pragma unroll
   for (int s = 0; s < 4; ++s)
     qf[s] = my_q < p.Lq ? *(const bf16x8*)(Q + my_q * p.ldq + 16 * s + 8 * h) : bf16x8{};
+  if constexpr (BOUNDED) {
+    // q' = bf16(q * c), c = scale * log2(e): S' = K q'^T is already the exp2 argument.  With
+    // |q.k| <= bound, |S'| <= c * bound (checked < 40 on the host), so p = exp2(S') needs no
+    // running max and no offset; the one extra rounding of q' is 2^-9 relative per element.
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float f[8];
+      unpack8(qf[s], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= p.scale_log2;
+      qf[s] = pack8(f);
+    }
+  }
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const bool wave_live = r0 < p.Lq;
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
@@ -118,10 +130,11 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   f32x16 o[2];
   o[0] = f32x16{};
   o[1] = f32x16{};
-  float mrow = BOUNDED ? p.bound : -INFINITY, lrow = 0.f;
+  float mrow = BOUNDED ? 0.f : -INFINITY, lrow = 0.f;
 
   constexpr int BUFB = 2 * KT * D * 2;
   bf16x8 kr[2], vr[2];
+  const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_TR>(p.ldv, w, lane);
   if (GLDS) {
     if (ntiles > 0) {
       tile_glds<SW_ROW>(smem, K, p.ldk, kv_begin, p.Lkv, w, lane);
@@ -152,8 +165,14 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
     if (GLDS) {
       if (more2) {
         char* nb = smem + ((t + 2) % 3) * BUFB;
-        tile_glds<SW_ROW>(nb, K, p.ldk, c0 + 2 * KT, p.Lkv, w, lane);
-        tile_glds<SW_TR>(nb + KT * D * 2, V, p.ldv, c0 + 2 * KT, p.Lkv, w, lane);
+        const long c2 = c0 + 2 * KT;
+        if (c2 + KT <= p.Lkv) {
+          tile_glds_fast(nb, K + c2 * p.ldk, goff_k, w);
+          tile_glds_fast(nb + KT * D * 2, V + c2 * p.ldv, goff_v, w);
+        } else {
+          tile_glds<SW_ROW>(nb, K, p.ldk, c2, p.Lkv, w, lane);
+          tile_glds<SW_TR>(nb + KT * D * 2, V, p.ldv, c2, p.Lkv, w, lane);
+        }
       }
     } else if (more) {
       stage_load(kr, K, p.ldk, c0 + KT, p.Lkv);
@@ -187,10 +206,8 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
         apply_bits<0>(st[0], bh, -INFINITY);
         apply_bits<32>(st[1], bh, -INFINITY);
       }
-      float mc;
-      if constexpr (BOUNDED) {
-        mc = mrow * p.scale_log2;
-      } else {
+      float mc = 0.f;
+      if constexpr (!BOUNDED) {
         // row max on raw scores; p = exp2(s * c - m * c) is one FMA + one v_exp per score
         float tmax = -INFINITY;
 #pragma unroll
@@ -215,7 +232,8 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(st[kb][r], p.scale_log2, -mc));
+          const float pv = BOUNDED ? __builtin_amdgcn_exp2f(st[kb][r])
+                                   : __builtin_amdgcn_exp2f(fmaf(st[kb][r], p.scale_log2, -mc));
           st[kb][r] = pv;
           psum += pv;
         }
@@ -306,7 +324,7 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
   p.Lq = Lq; p.Lkv = Lkv; p.H = H;
   p.scale_log2 = scale * LOG2E;
   p.bound = score_bound;
-  OWLK_REQUIRE(score_bound >= 0.f && score_bound * scale < 64.f, "attn_fwd: score_bound out of range");
+  OWLK_REQUIRE(score_bound >= 0.f && score_bound * scale < 40.f, "attn_fwd: score_bound out of range");
   p.m = owlk_make_mask(tpf, window, causal, q_offset, Lkv, kv_lo, q_hi, run_start, doc, fstride);
   dim3 grid((unsigned)((Lq + QT - 1) / QT), (unsigned)H, (unsigned)B);
   static const int variant = getenv("OWLK_ATTN_FWD_REGSTAGE") ? 0 : 1;

@@ -187,8 +187,9 @@ def test_attention_fwd_bwd(case):
 
 @pytest.mark.parametrize("case", [ATTN_CASES[0], ATTN_CASES[2], ATTN_CASES[4], ATTN_CASES[6]])
 def test_attention_fwd_score_bound(case):
-    """Fixed-offset softmax (score_bound) on QK-RMSNorm'd inputs == oracle, and its lse equals
-    the running-max kernel's (softmax is shift invariant; only rounding differs)."""
+    """Bounded softmax (score_bound: p = exp2(c s) with q prescaled by c in-kernel) on
+    QK-RMSNorm'd inputs == oracle; its lse equals the running-max kernel's up to the one extra
+    bf16 rounding of q' = q c (2^-9 relative per element -> measured <= 1.4e-3 in lse)."""
     k = K()
     B, H, nf, tpf, window, docs = case
     L, D = nf * tpf, 64
@@ -205,7 +206,7 @@ def test_attention_fwd_score_bound(case):
     ref = R.attention(*(t.cpu().float().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v)),
                       R.frame_mask(L, L, tpf, window, doc if docs else None))
     assert rel(o.view(B, L, H, D).transpose(1, 2), ref) < 1e-2
-    assert (lse - lse0).abs().max().item() < 1e-4
+    assert (lse - lse0).abs().max().item() < 3e-3
     assert rel(o, o0) < 5e-3
 
 

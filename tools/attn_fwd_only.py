@@ -13,9 +13,11 @@ H, D, tpf, nf = 24, 64, 64, int(os.environ.get("FRAMES", "512"))
 L = nf * tpf
 torch.manual_seed(0)
 qkv = torch.randn(1, L, 3 * H * D, device="cuda", dtype=torch.bfloat16)
+qk = qkv[:, :, :2 * H * D].view(1, L, 2 * H, D)  # QK-RMSNorm'd, as in the model
+qk.copy_((qk.float() * torch.rsqrt(qk.float().pow(2).mean(-1, keepdim=True))).bfloat16())
 q, k, v = qkv[:, :, :H * D], qkv[:, :, H * D:2 * H * D], qkv[:, :, 2 * H * D:]
 mask = K.FrameMask(tpf, None)
-o, lse = K.attn_fwd(q, k, v, H, D, mask)
+o, lse = K.attn_fwd(q, k, v, H, D, mask, score_bound=K.qk_norm_bound(D))
 if which == "bwd":
     do = torch.randn_like(o)
     dq, dk, dv = (torch.empty_like(o) for _ in range(3))
