@@ -4,6 +4,7 @@
 // template): with P recomputed from the forward log-sum-exp,
 //   dV = P^T dO,  dS = P o (dP - delta),  dP = dO V^T,  delta = rowsum(dO o O),
 //   dK = scale * dS^T Q,  dQ = scale * dS K.
+// lse is the forward's base-2 log-sum-exp of the scaled logits, so P = exp2(c s - lse).
 // Two deterministic kernels (no float atomics):
 //   dkdv : workgroup = 4 waves x 32 keys; sweeps 64-query tiles; S, dP with the key on the lane
 //          (Q/dO rows x K/V in registers), then dV^T += dO^T P and dK^T += Q^T dS take P / dS
@@ -52,9 +53,9 @@ DEV void store_rowT(bf16* dst, const f32x16 (&acc)[2], float mul, int h) {
 __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) {
   constexpr int TILE = TL * D * 2;                     // 8 KiB
   constexpr int BUF = 2 * TILE + 2 * TL * 4;           // Q | dO | lse2 | delta
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem[3 * BUF];
   __shared__ int red_hi;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const long b = blockIdx.z;
   const int head = blockIdx.y;
@@ -106,36 +107,43 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
   f32x16 dk[2], dv[2];
   dk[0] = dk[1] = dv[0] = dv[1] = f32x16{};
 
-  bf16x8 qr[2], dr[2];
-  float lr = 0.f, dl = 0.f;
-  auto load = [&](long q0) {
-    tile_load(qr, Q, p.ldq, q0, p.Lq);
-    tile_load(dr, dO, p.ldo, q0, p.Lq);
-    if (threadIdx.x < TL) {
-      const long qi = q0 + threadIdx.x;
-      lr = qi < p.Lq ? LSE[qi] * LOG2E : 0.f;
-      dl = qi < p.Lq ? DLT[qi] : 0.f;
+  // Q / dO tiles + the lse2 / delta rows arrive by LDS-DMA into a 3-deep ring, two tiles in
+  // flight: per tile every wave issues 4 x 1 KiB (its 16 rows of Q and dO) and waves 0 / 1 one
+  // 256-B row each (lse2 / delta); offsets are per-lane constants, bases wave-uniform.
+  const GldsOff go_q = glds_offsets<SW_DUAL>(p.ldq, w, lane), go_d = glds_offsets<SW_DUAL>(p.ldo, w, lane);
+  auto issue = [&](char* buf, long q0) {
+    const bool inner = q0 + TL <= p.Lq;
+    if (inner) {
+      tile_glds_fast(buf, Q + q0 * p.ldq, go_q, w);
+      tile_glds_fast(buf + TILE, dO + q0 * p.ldo, go_d, w);
+    } else {
+      tile_glds<SW_DUAL>(buf, Q, p.ldq, q0, p.Lq, w, lane);
+      tile_glds<SW_DUAL>(buf + TILE, dO, p.ldo, q0, p.Lq, w, lane);
+    }
+    if (w < 2) {
+      const long n = p.Lq - q0;
+      const int i = inner ? lane : (lane < n ? lane : (int)n - 1);  // ragged tail: clamp (masked later)
+      glds_f32(buf + 2 * TILE + w * TL * 4, (w == 0 ? LSE : DLT) + q0 + i);
     }
   };
-  auto store = [&](char* buf) {
-    tile_store<SW_DUAL>(buf, qr);
-    tile_store<SW_DUAL>(buf + TILE, dr);
-    if (threadIdx.x < TL) {
-      ((float*)(buf + 2 * TILE))[threadIdx.x] = lr;
-      ((float*)(buf + 2 * TILE + TL * 4))[threadIdx.x] = dl;
-    }
+  auto wait_next = [&](bool two_in_flight) {  // this wave's share of the older tile has landed
+    if (!two_in_flight)
+      OWLK_VMCNT(0);
+    else if (w < 2)
+      OWLK_VMCNT(5);
+    else
+      OWLK_VMCNT(4);
   };
-  if (ntiles > 0) {
-    load(qbeg);
-    store(smem);
-  }
-  __syncthreads();
+  if (ntiles > 0) issue(smem, qbeg);
+  if (ntiles > 1) issue(smem + BUF, qbeg + TL);
+  wait_next(ntiles > 1);
+  OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
     const long q0 = qbeg + (long)t * TL;
-    const bool more = t + 1 < ntiles;
-    if (more) load(q0 + TL);
-    const char* lq = smem + (t & 1) * BUF;
+    const bool more2 = t + 2 < ntiles;
+    if (more2) issue(smem + ((t + 2) % 3) * BUF, q0 + 2 * TL);
+    const char* lq = smem + (t % 3) * BUF;
     const char* ld = lq + TILE;
     const float* l2 = (const float*)(lq + 2 * TILE);
     const float* dlt = (const float*)(lq + 2 * TILE + TL * 4);
@@ -191,8 +199,8 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
         }
       }
     }
-    if (more) store(smem + ((t + 1) & 1) * BUF);
-    __syncthreads();
+    wait_next(more2);
+    OWLK_BARRIER();
   }
 
   if (my_k < p.Lkv) {
@@ -205,9 +213,9 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
   constexpr int TILE = TL * D * 2;
   constexpr int BUF = 2 * TILE;  // K | V
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) char smem[3 * BUF];
   __shared__ int red_lo;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const long b = blockIdx.z;
   const int head = blockIdx.y;
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
     qf[s] = qok ? *(const bf16x8*)(Q + my_q * p.ldq + 16 * s + 8 * h) : bf16x8{};
     df[s] = qok ? *(const bf16x8*)(dO + my_q * p.ldo + 16 * s + 8 * h) : bf16x8{};
   }
-  const float L2 = qok ? p.lse[(b * p.H + head) * p.Lq + my_q] * LOG2E : 0.f;
+  const float L2 = qok ? p.lse[(b * p.H + head) * p.Lq + my_q] : 0.f;  // base-2 lse (attn_fwd)
   const float Dl = qok ? p.delta[(b * p.H + head) * p.Lq + my_q] : 0.f;
   const bool wave_live = r0 < p.Lq;
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
@@ -258,23 +266,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
 
   f32x16 dq[2];
   dq[0] = dq[1] = f32x16{};
-  bf16x8 kr[2], vr[2];
-  if (ntiles > 0) {
-    tile_load(kr, K, p.ldk, kv_begin, p.Lkv);
-    tile_load(vr, V, p.ldv, kv_begin, p.Lkv);
-    tile_store<SW_DUAL>(smem, kr);
-    tile_store<SW_ROW>(smem + TILE, vr);
+  // K / V tiles by LDS-DMA into a 3-deep ring (as in the forward), two tiles in flight
+  const GldsOff go_k = glds_offsets<SW_DUAL>(p.ldk, w, lane), go_v = glds_offsets<SW_ROW>(p.ldv, w, lane);
+  auto issue = [&](char* buf, long c0) {
+    if (c0 + TL <= p.Lkv) {
+      tile_glds_fast(buf, K + c0 * p.ldk, go_k, w);
+      tile_glds_fast(buf + TILE, V + c0 * p.ldv, go_v, w);
+    } else {
+      tile_glds<SW_DUAL>(buf, K, p.ldk, c0, p.Lkv, w, lane);
+      tile_glds<SW_ROW>(buf + TILE, V, p.ldv, c0, p.Lkv, w, lane);
+    }
+  };
+  if (ntiles > 0) issue(smem, kv_begin);
+  if (ntiles > 1) {
+    issue(smem + BUF, kv_begin + TL);
+    OWLK_VMCNT(4);
+  } else {
+    OWLK_VMCNT(0);
   }
-  __syncthreads();
+  OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
     const long c0 = kv_begin + (long)t * TL;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      tile_load(kr, K, p.ldk, c0 + TL, p.Lkv);
-      tile_load(vr, V, p.ldv, c0 + TL, p.Lkv);
-    }
-    const char* lk = smem + (t & 1) * BUF;
+    const bool more2 = t + 2 < ntiles;
+    if (more2) issue(smem + ((t + 2) % 3) * BUF, c0 + 2 * TL);
+    const char* lk = smem + (t % 3) * BUF;
     const char* lv = lk + TILE;
     const long clast = (c0 + TL - 1 < p.Lkv ? c0 + TL - 1 : p.Lkv - 1);
     int kind = TILE_EMPTY;
@@ -314,12 +330,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
         }
       }
     }
-    if (more) {
-      char* nb = smem + ((t + 1) & 1) * BUF;
-      tile_store<SW_DUAL>(nb, kr);
-      tile_store<SW_ROW>(nb + TILE, vr);
-    }
-    __syncthreads();
+    if (more2)
+      OWLK_VMCNT(4);
+    else
+      OWLK_VMCNT(0);
+    OWLK_BARRIER();
   }
   if (qok) store_rowT(p.dq + b * p.sdqb + my_q * p.lddq + head * D, dq, p.scale, h);
 }

@@ -210,6 +210,12 @@ DEV void tile_glds_fast(char* lds, const bf16* tile_base, const GldsOff& g, int 
                                      0, 0);
 }
 
+// one 64-float row by one wave-instruction (4 B per lane, lane-linear in LDS)
+DEV void glds_f32(char* lds_row, const float* src) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds_row, 4, 0, 0);
+}
+
 #define OWLK_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #define OWLK_BARRIER() asm volatile("s_barrier" ::: "memory")
 

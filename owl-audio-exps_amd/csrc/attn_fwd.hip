@@ -9,7 +9,9 @@
 // tile the wave computes S^T = K Q^T with v_mfma_f32_32x32x16_bf16 (key rows in registers, the
 // query on the lane) so the softmax row statistics stay in-lane (+ one lane^32 exchange), then
 // feeds the S^T accumulators straight back as the B operand of O^T += V^T P^T (V^T fragments
-// through ds_read_b64_tr_b16).  K/V tiles are register-staged into a double-buffered LDS ring.
+// through ds_read_b64_tr_b16).  K/V tiles arrive by LDS-DMA into a 3-deep ring.
+// lse is written in base 2 of the scaled logits, lse2 = log2 sum_k exp2(scale log2(e) s_k) (=
+// natural lse * log2 e): the backward's P = exp2(c s - lse2) then needs no conversion.
 #include "attn_common.hpp"
 
 #include <cstdlib>
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
         *(bf16x4*)(O + 32 * db + 8 * gq + 4 * h) = v4;
       }
     if (h == 0)
-      p.lse[(b * p.H + head) * p.Lq + my_q] = ltot > 0.f ? mrow * p.scale_log2 * LN2 + __logf(ltot) : -INFINITY;
+      p.lse[(b * p.H + head) * p.Lq + my_q] = ltot > 0.f ? mrow * p.scale_log2 + __log2f(ltot) : -INFINITY;
   }
 }
 

@@ -177,6 +177,10 @@ def test_attention_fwd_bwd(case):
     m = R.frame_mask(L, L, tpf, window, doc if docs else None)
     oref = R.attention(qr, kr, vr, m)
     assert rel(o.view(B, L, H, D).transpose(1, 2), oref) < 1e-2
+    # lse (internal fwd -> bwd contract) is base 2: lse2 = log2 sum exp(s / sqrt(D))
+    sc = (qr.detach() @ kr.detach().transpose(-1, -2)) * D ** -0.5
+    lref = torch.logsumexp(sc.masked_fill(~m[:, None], float("-inf")), -1) / torch.log(torch.tensor(2.0))
+    assert (lse.cpu() - lref).abs().max().item() < 2e-2
     do = rnd(B * L, H * D, seed=43).view(B, L, H * D)
     oref.backward(do.cpu().float().view(B, L, H, D).transpose(1, 2))
     dq, dk, dv = (torch.empty_like(q) for _ in range(3))
@@ -189,7 +193,7 @@ def test_attention_fwd_bwd(case):
 def test_attention_fwd_score_bound(case):
     """Bounded softmax (score_bound: p = exp2(c s) with q prescaled by c in-kernel) on
     QK-RMSNorm'd inputs == oracle; its lse equals the running-max kernel's up to the one extra
-    bf16 rounding of q' = q c (2^-9 relative per element -> measured <= 1.4e-3 in lse)."""
+    bf16 rounding of q' = q c (2^-9 relative per element -> measured <= 2.1e-3 in lse2)."""
     k = K()
     B, H, nf, tpf, window, docs = case
     L, D = nf * tpf, 64
@@ -206,7 +210,7 @@ def test_attention_fwd_score_bound(case):
     ref = R.attention(*(t.cpu().float().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v)),
                       R.frame_mask(L, L, tpf, window, doc if docs else None))
     assert rel(o.view(B, L, H, D).transpose(1, 2), ref) < 1e-2
-    assert (lse - lse0).abs().max().item() < 3e-3
+    assert (lse - lse0).abs().max().item() < 4e-3
     assert rel(o, o0) < 5e-3
 
 
