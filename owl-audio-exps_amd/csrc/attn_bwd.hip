@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 }
 
 // ======================================================================== dQ
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(BwdP p) {
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(BwdP p) {
   constexpr int TILE = TL * D * 2;
   constexpr int BUF = 2 * TILE;  // K | V
   __shared__ __attribute__((aligned(16))) char smem[3 * BUF];
