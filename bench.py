@@ -177,6 +177,16 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
                 "launches_per_microstep": n, "avg_launch_ms": round(ms / n, 4),
                 "share_of_microstep_kernel_time": round(ms / tot_ms, 3)}
+        # HBM bytes per launch of the same kernel on this same command, from the committed PMC passes
+        # (tools/pmc_traffic.sh -> tools/traffic_summary.py -> profiles/<round>_traffic.json)
+        import glob
+        tf = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
+        if tf:
+            rec = json.load(open(tf[-1])).get(dom)
+            if rec:
+                roof["traffic"] = round(rec["traffic_bytes_per_launch"])
+                roof["traffic_unit"] = "bytes/launch (HBM, PMC)"
+                roof["traffic_source"] = os.path.relpath(tf[-1], REPO)
         if rank == 0:
             log("[bench] per-kernel time in one micro-step (ms):")
             for k, (n, ms_, fl_) in kernels[:40]:

@@ -122,6 +122,19 @@ int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, v
 int owlk_ns_normalize(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
                       float* work, void* stream);
 
+/* ---- MMDiT plumbing (frames.hip) ----
+ * owlk_frame_mux replaces the per-frame concat / split of mmattn.py:54-60 and :77-80: frame f of
+ * the joint sequence is [n0 rows of a (video) | n1 rows of b (audio)].  dir 0: a, b -> joint;
+ * dir 1: joint -> a, b.  `frames` counts frames over the whole batch; cols % 8 == 0 (bf16). */
+int owlk_frame_mux(int dir, long frames, int n0, int n1, int cols, void* a, long lda, void* b, long ldb,
+                   void* joint, long ldj, void* stream);
+/* F.layer_norm(x, (d,)) without affine, eps 1e-5, fp32 math, bf16 in/out (normalization.py:6-7,
+ * used on the MMDiT video head, gamerft_audio.py:89); mean / rstd fp32 [T] saved for backward */
+int owlk_layernorm_fwd(const void* x, long ldx, long T, int d, void* y, long ldy, float* mean, float* rstd,
+                       void* stream);
+int owlk_layernorm_bwd(const void* dy, long lddy, const void* x, long ldx, const float* mean, const float* rstd,
+                       long T, int d, void* dx, long lddx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,8 +48,10 @@ def rope_tables(cfg):
                                    getattr(cfg, "rope_base", 10000.0), has_audio=cfg.has_audio)
     elif impl == "audio1d":
         ang = R.audio1d_rope_angles(cfg.n_frames, D)
-    else:
-        raise NotImplementedError("OrthoRoPE (rotary-embedding-torch 'pixel' freqs) is parity-unpinned")
+    else:  # OrthoRoPE: parity-unpinned restatement of rotary-embedding-torch (ref_ops)
+        ang = R.ortho_rope_angles(cfg.n_frames, cfg.sample_size, D)
+        if not cfg.has_audio:
+            ang = ang.view(cfg.n_frames, -1, ang.shape[-1])[:, :-1].flatten(0, 1)
     return ang.cos().contiguous(), ang.sin().contiguous()
 
 
@@ -249,6 +251,119 @@ class AudioRFT(nn.Module):  # audiorft.py:13-93
         h = c.transformer(c.proj_in(xt), cond, doc_id)
         pred = c.proj_out(h, cond)
         return F.mse_loss(pred, target), pred
+
+
+# ----------------------------------------------------------------------------- MMDiT
+class _MMAttn(nn.Module):  # mmattn.py:28-86
+    def __init__(self, cfg):
+        super().__init__()
+        d = cfg.d_model
+        self.h = cfg.n_heads
+        self.n = [cfg.sample_size ** 2, 1]
+        self.qkv_projs = nn.ModuleList([nn.Linear(d, 3 * d) for _ in range(2)])
+        self.out_projs = nn.ModuleList([nn.Linear(d, d) for _ in range(2)])
+
+    def forward(self, x0, x1, mask, cos, sin):
+        B, d = x0.shape[0], x0.shape[-1]
+        # per-modality qkv, concatenated per frame: frame f = [n0 video | n1 audio] (mmattn.py:54-60)
+        parts = [self.qkv_projs[i](x).view(B, -1, self.n[i], 3 * d) for i, x in enumerate((x0, x1))]
+        qkv = torch.cat(parts, 2).reshape(B, -1, 3 * d)
+        L = qkv.shape[1]
+        q, k, v = qkv.view(B, L, 3, self.h, d // self.h).permute(2, 0, 3, 1, 4)
+        q, k = R.rms_norm(q), R.rms_norm(k)
+        q, k = R.rope_apply(q, cos, sin, 0), R.rope_apply(k, cos, sin, 0)
+        o = R.attention(q, k, v, mask).permute(0, 2, 1, 3).reshape(B, -1, self.n[0] + self.n[1], d)
+        o0, o1 = o[:, :, :self.n[0]].reshape(B, -1, d), o[:, :, self.n[0]:].reshape(B, -1, d)
+        return self.out_projs[0](o0), self.out_projs[1](o1)
+
+
+class _MMBlock(nn.Module):  # mmattn.py:89-114
+    def __init__(self, cfg):
+        super().__init__()
+        d = cfg.d_model
+        self.attn = _MMAttn(cfg)
+        self.mlps = nn.ModuleList([_MLP(d, 4 * d, d) for _ in range(2)])
+
+    def forward(self, x0, x1, c0, c1, mask, cos, sin):
+        m0, m1 = c0.chunk(6, dim=-1), c1.chunk(6, dim=-1)
+        h0, h1 = self.attn(R.cond_adaln(x0, m0[0], m0[1]), R.cond_adaln(x1, m1[0], m1[1]), mask, cos, sin)
+        x0, x1 = x0 + R.cond_gate(h0, m0[2]), x1 + R.cond_gate(h1, m1[2])
+        h0 = self.mlps[0](R.cond_adaln(x0, m0[3], m0[4]))
+        h1 = self.mlps[1](R.cond_adaln(x1, m1[3], m1[4]))
+        return x0 + R.cond_gate(h0, m0[5]), x1 + R.cond_gate(h1, m1[5])
+
+
+class MMDIT(nn.Module):  # mmattn.py:117-152 (modulation shared by all layers, DiT-Air)
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        d = cfg.d_model
+        self.local_layers = [(i % 4 != 0) for i in range(cfg.n_layers)]
+        self.blocks = nn.ModuleList([_MMBlock(cfg) for _ in range(cfg.n_layers)])
+        self.cond_proj = nn.Sequential(nn.SiLU(), nn.Linear(d, d * 2 * 2 * 3))
+        cos, sin = rope_tables(cfg)
+        self.register_buffer("cos", cos, persistent=False)
+        self.register_buffer("sin", sin, persistent=False)
+
+    def forward(self, x0, x1, cond):
+        L = x0.shape[1] + x1.shape[1]
+        tpf = self.cfg.tokens_per_frame
+        lm = gm = None
+        if self.cfg.causal:  # create_causal_block_mask, reconstructed
+            lm = R.frame_mask(L, L, tpf, self.cfg.local_window)
+            gm = R.frame_mask(L, L, tpf, self.cfg.global_window)
+        c0, c1 = self.cond_proj(cond).chunk(2, dim=-1)
+        for i, blk in enumerate(self.blocks):
+            x0, x1 = blk(x0, x1, c0, c1, lm if self.local_layers[i] else gm, self.cos, self.sin)
+        return x0, x1
+
+
+class GameRFTAudioCore(nn.Module):  # gamerft_audio.py:19-97 (mmdit backbone)
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        d = cfg.d_model
+        self.transformer = MMDIT(cfg)
+        if not cfg.uncond:
+            self.control_embed = _Control(cfg.n_buttons, d)
+        self.t_embed = _TEmbed(d)
+        self.proj_in = nn.Linear(cfg.channels, d, bias=False)
+        self.proj_out = _Final(d, cfg.channels)
+        self.audio_proj_in = nn.Linear(cfg.audio_channels, d, bias=False)
+        self.audio_proj_out = _Final(d, cfg.audio_channels)
+
+    def forward(self, x, audio, t, mouse, btn, has_controls=None):
+        cond = self.t_embed(t)
+        if not self.cfg.uncond:
+            ctrl = self.control_embed(mouse, btn)
+            if has_controls is not None:
+                ctrl = torch.where(has_controls[:, None, None], ctrl, torch.zeros_like(ctrl))
+            cond = cond + ctrl
+        b, n, c, h, w = x.shape
+        x = self.proj_in(x.permute(0, 1, 3, 4, 2).reshape(b, n * h * w, c))
+        video, aud = self.transformer(x, self.audio_proj_in(audio), cond)
+        video = self.proj_out(R.layer_norm(video), R.layer_norm(cond))
+        video = video.reshape(b, n, h, w, c).permute(0, 1, 4, 2, 3)
+        return video, self.audio_proj_out(aud, cond)
+
+
+class GameRFTAudio(nn.Module):  # gamerft_audio.py:99-178
+    def __init__(self, cfg):
+        super().__init__()
+        self.config = cfg
+        self.core = GameRFTAudioCore(cfg)
+
+    def forward(self, x, audio, mouse, btn, noise, cfg_prob=None):
+        B = x.shape[0]
+        hc = GameRFT.handle_cfg(torch.ones(B, dtype=torch.bool), self.config.cfg_prob if cfg_prob is None
+                                else cfg_prob, noise["rand_b"])
+        with torch.no_grad():
+            ts = noise["ts_raw"].to(x.dtype).sigmoid()
+            xt, tv = R.flow_noise(x, ts[:, :, None, None, None], noise["z_video"].to(x.dtype))
+            at, ta = R.flow_noise(audio, ts[:, :, None], noise["z_audio"].to(audio.dtype))
+        pv, pa = self.core(xt, at, ts, mouse, btn, hc)
+        lv, la = F.mse_loss(pv, tv), F.mse_loss(pa, ta)
+        return lv + la, lv, la, pv, pa, hc
 
 
 # ----------------------------------------------------------------------------- optimizer

@@ -99,6 +99,28 @@ def audio1d_rope_angles(n_latents, d_head):
     return torch.arange(n_latents, dtype=torch.float32)[:, None] * lang_freqs(d_head)[None]
 
 
+def ortho_rope_angles(n_frames, sample_size, d_head, max_freq=256.0):
+    """rope.py:57-79 OrthoRoPE.  PARITY-UNPINNED: restates rotary-embedding-torch (absent, version
+    unpinned) 'pixel' freqs = linspace(1, max_freq/2, dim//2) * pi and get_axial_freqs (positions
+    linspace(-1, 1, n) + offset per axis, each freq repeated x2, axes broadcast and concatenated).
+    Returns [n_frames * (p*p + 1), d_head/2] (video tokens of a frame, then its audio token)."""
+    p = sample_size
+    dim = d_head // 4
+    freqs = torch.linspace(1.0, max_freq / 2, dim // 2) * math.pi
+    dims, offsets = (n_frames, p + 1, p + 1, 1), (0, 0, 0, 1)
+    axes = []
+    for i, (n, off) in enumerate(zip(dims, offsets)):
+        pos = torch.linspace(-1, 1, steps=n) + off
+        f = (pos[:, None] * freqs[None]).repeat_interleave(2, dim=-1)
+        shape = [1] * len(dims) + [f.shape[-1]]
+        shape[i] = n
+        axes.append(f.view(shape))
+    full = torch.cat(torch.broadcast_tensors(*axes), dim=-1).view(n_frames, p + 1, p + 1, -1)
+    vid = full[:, :p, :p].reshape(n_frames, p * p, -1)
+    aud = full[:, -1, -1].unsqueeze(1)
+    return torch.cat([vid, aud], dim=1).flatten(0, 1)[..., ::2]
+
+
 def rope_apply(x, cos, sin, offset=0):
     """rope.py:43-51: fp32 pairwise rotation, output laid out [rot_even || rot_odd], cast back."""
     L = x.shape[-2]

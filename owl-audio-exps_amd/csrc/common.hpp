@@ -77,4 +77,22 @@ int check_launch(const char* what);
       return 1;                             \
     }                                       \
   } while (0)
+
+static constexpr int MAXCPL = 8;  // max 16-B chunks per lane (d <= 4096)
+
+// launch helper: pick the chunks-per-lane instantiation for a row width d
+#define OWLK_CPL_DISPATCH(d, KERNEL, ...)                     \
+  do {                                                        \
+    const int cpl_ = ((d) / 8 + 63) / 64;                     \
+    switch (cpl_) {                                           \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break; \
+      case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break; \
+      case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break; \
+      case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break; \
+      case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
+      case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break; \
+      default: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break; \
+    }                                                         \
+  } while (0)
+
 #endif

@@ -9,22 +9,6 @@
 namespace {
 
 constexpr float RMS_EPS = 1.1920928955078125e-07f;  // finfo(float32).eps, F.rms_norm default
-constexpr int MAXCPL = 8;  // max 16-B chunks per lane (d <= 4096)
-
-// launch helper: pick the chunks-per-lane instantiation for a row width d
-#define OWLK_CPL_DISPATCH(d, KERNEL, ...)                     \
-  do {                                                        \
-    const int cpl_ = ((d) / 8 + 63) / 64;                     \
-    switch (cpl_) {                                           \
-      case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break; \
-      case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break; \
-      case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break; \
-      case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break; \
-      case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break; \
-      case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break; \
-      default: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break; \
-    }                                                         \
-  } while (0)
 
 // ------------------------------------------------------------------ AdaLN forward
 // one wave per token row; lane owns chunks c = lane + 64*i

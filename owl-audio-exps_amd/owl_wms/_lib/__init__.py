@@ -23,6 +23,9 @@ _SIGS = {
     "owlk_qk_rope_bwd": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P],
     "owlk_attn_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, L, I, F, F, L, I, I, L, P, P, P, P, L, P],
     "owlk_attn_delta": [P, P, L, L, L, I, I, P, P],
+    "owlk_frame_mux": [I, L, I, I, I, P, L, P, L, P, L, P],
+    "owlk_layernorm_fwd": [P, L, L, I, P, L, P, P, P],
+    "owlk_layernorm_bwd": [P, L, P, L, P, P, L, I, P, L, P],
     "owlk_attn_bwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I, I,
                       P, P, P, P, L, P],
     "owlk_attn_bwd_dkdv": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I,

@@ -293,3 +293,49 @@ def ns_normalize(g, transpose, work=None):
     g = g.contiguous()
     call("owlk_ns_normalize", ptr(g), int(g.dtype == F32), r, c, b, int(transpose), ptr(x), ptr(work), stream())
     return x
+
+
+# ---------------------------------------------------------------- MMDiT plumbing (frames.hip)
+def frame_interleave(a, b, n0, n1, out=None):
+    """a [F*n0, C], b [F*n1, C] token-major -> joint [F*(n0+n1), C] (frame f = a-rows | b-rows)."""
+    C = a.shape[1]
+    F_ = a.shape[0] // n0
+    assert a.shape[0] == F_ * n0 and b.shape[0] == F_ * n1 and b.shape[1] == C
+    if out is None:
+        out = torch.empty(F_ * (n0 + n1), C, device=a.device, dtype=BF16)
+    call("owlk_frame_mux", 0, F_, n0, n1, C, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out), out.stride(0),
+         stream(), key="frame_mux")
+    return out
+
+
+def frame_split(j, n0, n1, a=None, b=None):
+    """inverse of frame_interleave: joint [F*(n0+n1), C] -> (a [F*n0, C], b [F*n1, C])."""
+    C = j.shape[1]
+    F_ = j.shape[0] // (n0 + n1)
+    assert j.shape[0] == F_ * (n0 + n1)
+    if a is None:
+        a = torch.empty(F_ * n0, C, device=j.device, dtype=BF16)
+    if b is None:
+        b = torch.empty(F_ * n1, C, device=j.device, dtype=BF16)
+    call("owlk_frame_mux", 1, F_, n0, n1, C, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(j), j.stride(0),
+         stream(), key="frame_mux")
+    return a, b
+
+
+def layernorm_fwd(x):
+    """F.layer_norm(x, (d,)) (no affine, eps 1e-5) -> (y bf16, mean, rstd)."""
+    T, d = x.shape
+    y = torch.empty(T, d, device=x.device, dtype=BF16)
+    mean = torch.empty(T, device=x.device, dtype=F32)
+    rstd = torch.empty(T, device=x.device, dtype=F32)
+    call("owlk_layernorm_fwd", ptr(x), x.stride(0), T, d, ptr(y), y.stride(0), ptr(mean), ptr(rstd), stream(),
+         key="layernorm_fwd")
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd):
+    T, d = x.shape
+    dx = torch.empty(T, d, device=x.device, dtype=BF16)
+    call("owlk_layernorm_bwd", ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), T, d, ptr(dx),
+         dx.stride(0), stream(), key="layernorm_bwd")
+    return dx

@@ -171,3 +171,47 @@ def test_audio_trajectory():
         opt.step()
         opt.zero_grad(set_to_none=True)
         assert abs(loss.item() - ref[step].item()) < 2e-5, (step, loss.item(), ref[step].item())
+
+
+# ----------------------------------------------------------------------------- MMDiT (configs[3])
+MM = golden("mmdit_tiny.pt")
+
+
+def mmdit_cfg(**over):
+    c = dict(model_id="game_rft_audio", sample_size=8, channels=32, audio_channels=16, n_layers=2, n_heads=2,
+             d_model=128, tokens_per_frame=65, n_buttons=11, n_mouse_axes=2, cfg_prob=0.1, n_frames=6,
+             causal=True, uncond=False, backbone="mmdit", local_window=2, global_window=4, has_audio=True)
+    c.update(over)
+    return SimpleNamespace(**c)
+
+
+def test_mmdit_schema_and_ortho_rope():
+    """Reconstructed reference MMDiT: same state_dict schema; the OrthoRoPE
+    restatement (parity-unpinned: rotary-embedding-torch is absent) matches the table the
+    reconstruction used."""
+    m = M.GameRFTAudio(mmdit_cfg())
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == MM["mmdit.schema"]
+    close(m.core.transformer.cos, MM["mmdit.rope.cos"], 0, 0)
+    close(m.core.transformer.sin, MM["mmdit.rope.sin"], 0, 0)
+
+
+def test_mmdit_bf16_autocast_loss_pred_grads():
+    p = "mmdit.bf16."
+    m = det_init_(M.GameRFTAudio(mmdit_cfg()), base_seed=5000).train()
+    noise = {k: MM[p + "in." + k] for k in ("rand_b", "ts_raw", "z_video", "z_audio")}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        loss, lv, la, pv, pa, hc = m(MM[p + "in.x"], MM[p + "in.audio"], MM[p + "in.mouse"], MM[p + "in.btn"],
+                                     noise)
+    loss.backward()
+    assert torch.equal(hc, MM[p + "cfg_mask"])
+    for got, k in ((loss, "diffusion_loss"), (lv, "video_loss"), (la, "audio_loss")):
+        assert abs(got.item() - MM[p + k].item()) <= 1e-4 * MM[p + k].item(), k
+    close(pv, MM[p + "pred_video"], 2e-2, 2e-2)
+    close(pa, MM[p + "pred_audio"], 2e-2, 2e-2)
+    n = 0
+    for k, prm in m.named_parameters():
+        if p + "grad." + k in MM:
+            ref = MM[p + "grad." + k]
+            assert ((prm.grad.double() - ref.double()).norm() / ref.double().norm()).item() < 1e-2, k
+            n += 1
+    assert n >= 10
