@@ -32,7 +32,12 @@ class InjectedNoise:
         return self.d["ts_raw"].to(device=device, dtype=dtype)
 
     def z(self, x):
-        return self.d["z"].to(device=x.device, dtype=x.dtype)
+        z = self.d["z"]
+        if isinstance(z, (list, tuple)):  # several randn_like draws in order (video, then audio)
+            self._zi = getattr(self, "_zi", 0)
+            z = z[self._zi]
+            self._zi += 1
+        return z.to(device=x.device, dtype=x.dtype)
 
 
 def handle_cfg(has_controls, cfg_prob, noise):
@@ -62,3 +67,16 @@ def noised_tokens(x5, noise):
 
 def flow_loss(pred_tok, tgt_tok):
     return FlowLossFn.apply(pred_tok, tgt_tok)
+
+
+def noised_av(x5, a3, noise):
+    """gamerft_audio.py:137-151: one ts for both modalities; draw order ts -> z_video -> z_audio.
+    Returns token-major (xt, tgt, ts, z) for video and (at, atgt) for audio."""
+    B, N = x5.shape[:2]
+    xb, ab = x5.to(torch.bfloat16), a3.to(torch.bfloat16)
+    ts_raw = noise.ts_raw(B, N, xb.device, torch.bfloat16)
+    zv, za = noise.z(xb), noise.z(ab)
+    shp = xb.shape
+    xt, tgt, ts = K.flow_noise(xb.reshape(B, N, shp[2], -1, 1), zv.reshape(B, N, shp[2], -1, 1), ts_raw)
+    at, atgt, _ = K.flow_noise(ab.reshape(B, N, ab.shape[2], 1, 1), za.reshape(B, N, ab.shape[2], 1, 1), ts_raw)
+    return xt, tgt, ts, zv, at, atgt, za

@@ -206,6 +206,29 @@ class DiTBlockFn(torch.autograd.Function):
                 dwqkv, dbqkv, dwout, dbout, dw1, db1, dw2, db2, None)
 
 
+class LayerNormFn(torch.autograd.Function):
+    """F.layer_norm(x, (d,)).type_as(x) (normalization.py:6-7): fp32 math, bf16 out, libowlk."""
+
+    @staticmethod
+    def forward(ctx, x):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).to(BF16).contiguous()
+        y, mean, rstd = K.layernorm_fwd(x2)
+        ctx.save_for_backward(x2, mean, rstd)
+        ctx.shp, ctx.xdtype = shp, x.dtype
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, mean, rstd = ctx.saved_tensors
+        dx = K.layernorm_bwd(dy.reshape(x2.shape).to(BF16).contiguous(), x2, mean, rstd)
+        return dx.view(ctx.shp).to(ctx.xdtype)
+
+
+def layer_norm(x):
+    return LayerNormFn.apply(x)
+
+
 class FlowLossFn(torch.autograd.Function):
     """F.mse_loss(pred_tok, tgt_tok) with the gradient produced by the same kernel."""
 

@@ -8,8 +8,9 @@ import torch.nn.functional as F
 
 
 def layer_norm(x: torch.Tensor) -> torch.Tensor:
-    """normalization.py:6-7 (MMDiT head)."""
-    return F.layer_norm(x, (x.size(-1),)).type_as(x)
+    """normalization.py:6-7 (MMDiT head) on the libowlk layer_norm kernels."""
+    from .fused import layer_norm as _ln
+    return _ln(x)
 
 
 def rms_norm(x: torch.Tensor) -> torch.Tensor:

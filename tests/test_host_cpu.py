@@ -172,3 +172,18 @@ def test_reducer_and_muon_world_size_2():
         u = R.newton_schulz5(g2).float()
         exp = p * (1 - 0.1 * 0.01) - 0.1 * max(1, 8 / 12) ** 0.5 * u
         torch.testing.assert_close(muon[0][i], exp, rtol=1e-5, atol=1e-6)
+
+
+def test_mmdit_schema_matches_reconstructed_reference():
+    """GameRFTAudio (mmdit backbone) keys/shapes == the reconstructed reference's (mmdit_tiny.pt)."""
+    from conftest import golden
+    from owl_wms.configs import model_config
+    from owl_wms.models.gamerft_audio import GameRFTAudio
+    MM = golden("mmdit_tiny.pt")
+    cfg = model_config(model_id="game_rft_audio", sample_size=8, channels=32, audio_channels=16, n_layers=2,
+                       n_heads=2, d_model=128, tokens_per_frame=65, n_buttons=11, n_mouse_axes=2, cfg_prob=0.1,
+                       n_frames=6, causal=True, uncond=False, backbone="mmdit", local_window=2, global_window=4,
+                       has_audio=True)
+    m = GameRFTAudio(cfg)
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == MM["mmdit.schema"]
+    torch.testing.assert_close(m.core.transformer.rope.cos, MM["mmdit.rope.cos"], atol=0, rtol=0)

@@ -279,3 +279,29 @@ def test_gemm_splitk_weight_grad(M, N, K_):
     ref = dy.float().T @ x.float()
     out = k.gemm_wgrad(dy, x)
     assert rel(out, ref) < 1e-5
+
+
+def test_frame_mux_roundtrip():
+    """frame_interleave == per-frame torch.cat (mmattn.py:54-60); frame_split is its exact inverse."""
+    k = K()
+    F_, n0, n1, C = 7, 64, 1, 96
+    a, b = rnd(F_ * n0, C, seed=70), rnd(F_ * n1, C, seed=71)
+    j = k.frame_interleave(a, b, n0, n1)
+    ref = torch.cat([a.view(F_, n0, C), b.view(F_, n1, C)], 1).reshape(-1, C)
+    assert torch.equal(j, ref)
+    a2, b2 = k.frame_split(j, n0, n1)
+    assert torch.equal(a2, a) and torch.equal(b2, b)
+
+
+@pytest.mark.parametrize("T,d", [(300, 128), (130, 1536), (65, 2560)])
+def test_layernorm_fwd_bwd(T, d):
+    """normalization.py:6-7 under autocast: fp32 layer_norm (eps 1e-5) of bf16 x, rounded to bf16."""
+    k = K()
+    x = rnd(T, d, scale=3.0, seed=72)
+    y, mean, rstd = k.layernorm_fwd(x)
+    xr = x.float().cpu().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (d,))
+    assert (y.float().cpu() - yr.detach().bfloat16().float()).abs().max() <= 2 ** -7 * yr.abs().max()
+    dy = rnd(T, d, seed=73)
+    yr.backward(dy.float().cpu())
+    assert rel(k.layernorm_bwd(dy, x, mean, rstd), xr.grad) < 1e-2

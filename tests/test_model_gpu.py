@@ -175,3 +175,37 @@ def test_kv_cache_decode_matches_full_forward():
     # the tiny config's local window is 2 frames: decode keeps the last 2 frames of keys, exactly
     # what the mask allows the last frame to see in the full pass
     assert rel(last[:, 0], full[:, -1]) < 2e-2
+
+
+MMCFG = dict(model_id="game_rft_audio", sample_size=8, channels=32, audio_channels=16, n_layers=2, n_heads=2,
+             d_model=128, tokens_per_frame=65, n_buttons=11, n_mouse_axes=2, cfg_prob=0.1, n_frames=6, causal=True,
+             uncond=False, backbone="mmdit", local_window=2, global_window=4, has_audio=True)
+
+
+def test_mmdit_loss_pred_grads_vs_reference():
+    """BASELINE configs[3] path (two-stream MMDiT, tpf 65 joint attention, shared modulation) vs the
+    reconstructed reference (tests/golden/make_golden_mmdit.py), bf16 autocast semantics."""
+    from owl_wms.configs import model_config
+    from owl_wms.models.flow import InjectedNoise
+    from owl_wms.models.gamerft_audio import GameRFTAudio
+    MM = golden("mmdit_tiny.pt")
+    p = "mmdit.bf16."
+    m = det_init_(GameRFTAudio(model_config(**MMCFG)), base_seed=5000).cuda().train()
+    m.noise_source = InjectedNoise({"rand_b": MM[p + "in.rand_b"], "ts_raw": MM[p + "in.ts_raw"],
+                                    "z": [MM[p + "in.z_video"], MM[p + "in.z_audio"]]})
+    d = m(MM[p + "in.x"].cuda(), MM[p + "in.audio"].cuda(), MM[p + "in.mouse"].cuda(), MM[p + "in.btn"].cuda(),
+          return_dict=True)
+    d["diffusion_loss"].backward()
+    assert torch.equal(d["cfg_mask"].cpu(), MM[p + "cfg_mask"])
+    for k in ("diffusion_loss", "video_loss", "audio_loss"):
+        assert abs(d[k].item() - MM[p + k].item()) <= 5e-3 * MM[p + k].item(), (k, d[k].item(), MM[p + k].item())
+    assert rel(d["pred_video"], MM[p + "pred_video"]) < 2e-2
+    assert rel(d["pred_audio"], MM[p + "pred_audio"]) < 2e-2
+    n = 0
+    for i, (k, prm) in enumerate(sorted(m.named_parameters())):
+        st = MM[p + "gradstat." + k]
+        assert abs(prm.grad.double().norm().item() - st[3].item()) <= 5e-2 * st[3].item() + 1e-7, k
+        if p + "grad." + k in MM:
+            assert rel(prm.grad, MM[p + "grad." + k]) < 2e-2, (k, rel(prm.grad, MM[p + "grad." + k]))
+            n += 1
+    assert n >= 10
