@@ -1,0 +1,75 @@
+"""AVCachingSamplerV2 (reference: owl_wms/sampling/av_caching_v2.py:24-144) on libowlk.
+
+Context frames are cached once at noise level ``noise_prev``; each new frame starts from
+N(0, 1) at t = 1, takes ``n_steps`` Euler steps x -= dt_i v (optional CFG with null controls),
+is re-noised (zlerp) and appended to the cache.  In decode mode the attention is unmasked over
+[cache | new frame]; local layers keep the last local_window frames.  Noise is drawn with
+torch.randn_like in the reference's order (context zlerp, then per frame: x0, then zlerp).
+"""
+import torch
+
+from ..nn.kv_cache import KVCache
+from .schedulers import get_deltas, get_sd3_euler
+
+
+class AVCachingSamplerV2:
+    def __init__(self, n_steps: int = 16, cfg_scale: float = 1.3, num_frames: int = 60, noise_prev: float = 0.2,
+                 max_window=None, custom_schedule=None) -> None:
+        self.cfg_scale = cfg_scale
+        self.n_steps = n_steps
+        self.num_frames = num_frames
+        self.noise_prev = noise_prev
+        self.max_window = max_window
+        self.custom_schedule = custom_schedule
+
+    @staticmethod
+    def zlerp(x, alpha):
+        z = torch.randn_like(x)
+        return x * (1.0 - alpha) + z * alpha
+
+    @torch.no_grad()
+    def __call__(self, model, x, mouse, btn, compile_on_decode=False):
+        """model: a GameRFTCore ([b,n,c,h,w] latents, kv_cache API); returns [b, init+new, c, h, w]."""
+        batch_size, init_len = x.size(0), x.size(1)
+        if self.custom_schedule is None:
+            dt = get_sd3_euler(self.n_steps).to(device=x.device, dtype=x.dtype)
+        else:
+            dt = get_deltas(self.custom_schedule)
+        kv_cache = KVCache(model.config)
+        kv_cache.reset(batch_size)
+
+        latents = [x.clone()]
+        prev_x = x
+        prev_mouse, prev_btn = mouse[:, :init_len], btn[:, :init_len]
+        prev_x_noisy = self.zlerp(prev_x, self.noise_prev)
+        prev_t = prev_x.new_full((batch_size, prev_x.size(1)), self.noise_prev)
+        kv_cache.enable_cache_updates()
+        model(prev_x_noisy, prev_t, prev_mouse, prev_btn, kv_cache=kv_cache)
+        kv_cache.disable_cache_updates()
+
+        num_frames = min(self.num_frames, mouse.size(1) - init_len)
+        model.transformer.enable_decoding()
+        try:
+            for idx in range(num_frames):
+                curr_x, curr_t = torch.randn_like(prev_x[:, :1]), prev_t.new_ones(batch_size, 1)
+                start = init_len + idx
+                curr_mouse, curr_btn = mouse[:, start:start + 1], btn[:, start:start + 1]
+                null_mouse, null_btn = torch.zeros_like(curr_mouse), torch.zeros_like(curr_btn)
+                for t_idx in range(self.n_steps):
+                    pred_v = model(curr_x, curr_t, curr_mouse, curr_btn, kv_cache=kv_cache).clone()
+                    if self.cfg_scale != 1.0:
+                        pred_u = model(curr_x, curr_t, null_mouse, null_btn, kv_cache=kv_cache).clone()
+                        pred_v = pred_u + self.cfg_scale * (pred_v - pred_u)
+                    curr_x = curr_x - dt[t_idx] * pred_v
+                    curr_t = curr_t - dt[t_idx]
+                latents.append(curr_x.clone())
+                curr_x_noisy = self.zlerp(curr_x, self.noise_prev)
+                curr_t_noisy = torch.ones_like(curr_t) * self.noise_prev
+                kv_cache.enable_cache_updates()
+                model(curr_x_noisy, curr_t_noisy, curr_mouse, curr_btn, kv_cache=kv_cache)
+                kv_cache.disable_cache_updates()
+                if self.max_window is not None and len(latents) > self.max_window:
+                    kv_cache.truncate(1, front=False)
+        finally:
+            model.transformer.disable_decoding()
+        return torch.cat(latents, dim=1)

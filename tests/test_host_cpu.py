@@ -187,3 +187,15 @@ def test_mmdit_schema_matches_reconstructed_reference():
     m = GameRFTAudio(cfg)
     assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == MM["mmdit.schema"]
     torch.testing.assert_close(m.core.transformer.rope.cos, MM["mmdit.rope.cos"], atol=0, rtol=0)
+
+
+def test_sd3_euler_schedule():
+    """schedulers.py:5-13 restated (diffusers absent: parity-unpinned beyond this formula check):
+    sigma' = 3 s / (1 + 2 s), s = (N - i) / N, dt_i = sigma'_i - sigma'_{i+1}, sigma'_N = 0."""
+    from conftest import golden
+    from owl_wms.sampling.schedulers import get_deltas, get_sd3_euler
+    dt = get_sd3_euler(16)
+    assert dt.shape == (16,) and abs(dt.sum().item() - 1.0) < 1e-6
+    assert abs(dt[0].item() - (1 - 2.8125 / 2.875)) < 1e-6 and abs(dt[-1].item() - 0.1875 / 1.125) < 1e-6
+    torch.testing.assert_close(get_sd3_euler(2), golden("sampler_tiny.pt")["av.dt"], atol=0, rtol=0)
+    assert get_deltas([1.0, 0.5]) == [0.5, 0.5]

@@ -209,3 +209,56 @@ def test_mmdit_loss_pred_grads_vs_reference():
             assert rel(prm.grad, MM[p + "grad." + k]) < 2e-2, (k, rel(prm.grad, MM[p + "grad." + k]))
             n += 1
     assert n >= 10
+
+
+class _Draws:
+    """Replay torch.randn / randn_like draws (reference order) on the draw's device/dtype."""
+
+    def __init__(self, randn=(), like=()):
+        self.q = {"randn": list(randn), "like": list(like)}
+
+    def __enter__(self):
+        self.saved = (torch.randn, torch.randn_like)
+
+        def randn(*shape, device=None, dtype=None, **kw):
+            return self.q["randn"].pop(0).to(device=device, dtype=dtype or torch.float32)
+
+        def like(x, **kw):
+            return self.q["like"].pop(0).to(device=x.device, dtype=x.dtype)
+
+        torch.randn, torch.randn_like = randn, like
+        return self
+
+    def __exit__(self, *exc):
+        torch.randn, torch.randn_like = self.saved
+        assert not any(self.q.values()), "unconsumed draws"
+
+
+def test_av_caching_sampler_vs_reference():
+    """AVCachingSamplerV2 (av_caching_v2.py:24-144): 4 context frames + 3 generated, 2 Euler steps,
+    CFG 1.3, through the libowlk KV-cache decode path; sampled latents within 2e-2."""
+    from owl_wms.sampling import get_sampler_cls
+    S = golden("sampler_tiny.pt")
+    m = _model().eval()
+    sampler = get_sampler_cls("av_caching")(n_steps=2, cfg_scale=1.3, num_frames=3, noise_prev=0.2)
+    with _Draws(like=S["av.noise"]):
+        out = sampler(m.core, S["av.in.x"].cuda(), S["av.in.mouse"].cuda(), S["av.in.btn"].cuda())
+    assert out.shape == S["av.out"].shape
+    assert rel(out[:, :4], S["av.out"][:, :4]) == 0.0
+    assert rel(out[:, 4:], S["av.out"][:, 4:]) < 2e-2
+
+
+def test_audio_caching_sampler_vs_reference():
+    from owl_wms.configs import model_config
+    from owl_wms.models.audiorft import AudioRFT
+    from owl_wms.sampling import get_sampler_cls
+    S = golden("sampler_tiny.pt")
+    cfg = model_config(model_id="audio_rft", sample_size=120, channels=64, n_layers=2, n_heads=2, d_model=128,
+                       tokens_per_frame=1, n_frames=10000, cfg_prob=0.0, causal=True, uncond=True, backbone="dit",
+                       has_audio=True, rope_impl="audio1d", local_window=16, global_window=None)
+    m = det_init_(AudioRFT(cfg), base_seed=3000).cuda().eval()
+    sampler = get_sampler_cls("audio_caching")(n_steps=2, num_tokens=3, noise_prev=0.2)
+    with _Draws(randn=S["audio.noise_randn"], like=S["audio.noise_like"]):
+        out = sampler(m.core, S["audio.in.x"].cuda())
+    assert out.shape == S["audio.out"].shape
+    assert rel(out[:, 8:], S["audio.out"][:, 8:]) < 2e-2
