@@ -1,4 +1,4 @@
-// Block-sparse frame-causal flash attention, backward (gfx950, head_dim 64).
+// Block-sparse frame-causal flash attention, backward (gfx950, head_dim 64 and 128).
 //
 // Gradient of the reference's flex_attention (attn.py:106-109; autograd of torch's flex
 // template): with P recomputed from the forward log-sum-exp,
@@ -13,18 +13,25 @@
 //          lane), dQ^T += K^T dS^T with K^T fragments through ds_read_b64_tr_b16.
 #include "attn_common.hpp"
 
-#include <type_traits>
 
 namespace {
 
-constexpr int D = 64;
-constexpr int TB = 128;  // rows owned by a workgroup
-constexpr int TL = 64;   // rows per swept tile
+constexpr int TB = 128;              // rows owned by a workgroup (4 waves x 32)
+constexpr int TL = 64;               // rows per swept tile
+constexpr int SUB = TL * 64 * 2;     // one 64-row x 64-column bf16 sub-tile (128-B rows): 8 KiB
 constexpr float LOG2E = 1.4426950408889634f;
+
+// head_dim D as D/64 column sub-tiles (see attn_fwd.hip); ring depth 3 at D 64, 2 at D 128
+template <int D>
+struct Cfg {
+  static constexpr int NSUB = D / 64, NS = D / 16, NDB = D / 32;
+  static constexpr int NBUF = D == 64 ? 3 : 2;
+  static constexpr int OPS = 4 * NSUB;  // LDS-DMA wave-instructions per tile per wave (two tiles)
+};
 
 struct BwdP {
   const bf16 *q, *k, *v, *dout;
-  const float *lse, *delta;  // [B, H, Lq]
+  const float *lse, *delta;  // [B, H, Lq]; lse in base 2 (attn_fwd)
   bf16 *dq, *dk, *dv;
   long ldq, ldk, ldv, ldo, lddq, lddk, lddv;  // token row strides
   long sqb, skb, svb, sob, sdqb, sdkb, sdvb;  // batch strides
@@ -34,9 +41,15 @@ struct BwdP {
   MaskP m;
 };
 
-DEV void store_rowT(bf16* dst, const f32x16 (&acc)[2], float mul, int h) {
+template <int N>
+DEV void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NDB>
+DEV void store_rowT(bf16* dst, const f32x16 (&acc)[NDB], float mul, int h) {
 #pragma unroll
-  for (int db = 0; db < 2; ++db)
+  for (int db = 0; db < NDB; ++db)
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
       bf16x4 v4;
@@ -47,13 +60,11 @@ DEV void store_rowT(bf16* dst, const f32x16 (&acc)[2], float mul, int h) {
 }
 
 // ======================================================================== dK, dV
-#ifndef OWLK_DKDV_WAVES
-#define OWLK_DKDV_WAVES 2  // waves per SIMD the register allocation must allow
-#endif
-__global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) {
-  constexpr int TILE = TL * D * 2;                     // 8 KiB
-  constexpr int BUF = 2 * TILE + 2 * TL * 4;           // Q | dO | lse2 | delta
-  __shared__ __attribute__((aligned(16))) char smem[3 * BUF];
+template <int D>
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) {
+  using C = Cfg<D>;
+  constexpr int BUF = 2 * C::NSUB * SUB + 2 * TL * 4;  // Q | dO | lse2 | delta
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF];
   __shared__ int red_hi;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
@@ -93,60 +104,63 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
 
   // ---- this wave's K and V as B operands (key on the lane): X[key][16 s + 8 h ..]
   const long my_k = kw0 + ql;
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[C::NS], vf[C::NS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < C::NS; ++s) {
     kf[s] = my_k < p.Lkv ? *(const bf16x8*)(K + my_k * p.ldk + 16 * s + 8 * h) : bf16x8{};
     vf[s] = my_k < p.Lkv ? *(const bf16x8*)(V + my_k * p.ldv + 16 * s + 8 * h) : bf16x8{};
   }
   const bool wave_live = kw0 < p.Lkv;
   const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
   const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
-  const int my_fk = frame_of(m, my_k < p.Lkv ? my_k : wklast);
 
-  f32x16 dk[2], dv[2];
-  dk[0] = dk[1] = dv[0] = dv[1] = f32x16{};
+  f32x16 dk[C::NDB], dv[C::NDB];
+#pragma unroll
+  for (int db = 0; db < C::NDB; ++db) dk[db] = dv[db] = f32x16{};
 
-  // Q / dO tiles + the lse2 / delta rows arrive by LDS-DMA into a 3-deep ring, two tiles in
-  // flight: per tile every wave issues 4 x 1 KiB (its 16 rows of Q and dO) and waves 0 / 1 one
-  // 256-B row each (lse2 / delta); offsets are per-lane constants, bases wave-uniform.
+  // Q / dO tiles + the lse2 / delta rows arrive by LDS-DMA into the ring: per tile every wave
+  // issues 2 x 1 KiB per sub-tile of Q and of dO (its 16 rows), waves 0 / 1 one 256-B row each
+  // (lse2 / delta); offsets are per-lane constants, bases wave-uniform.
   const GldsOff go_q = glds_offsets<SW_DUAL>(p.ldq, w, lane), go_d = glds_offsets<SW_DUAL>(p.ldo, w, lane);
   auto issue = [&](char* buf, long q0) {
     const bool inner = q0 + TL <= p.Lq;
-    if (inner) {
-      tile_glds_fast(buf, Q + q0 * p.ldq, go_q, w);
-      tile_glds_fast(buf + TILE, dO + q0 * p.ldo, go_d, w);
-    } else {
-      tile_glds<SW_DUAL>(buf, Q, p.ldq, q0, p.Lq, w, lane);
-      tile_glds<SW_DUAL>(buf + TILE, dO, p.ldo, q0, p.Lq, w, lane);
+#pragma unroll
+    for (int sb = 0; sb < C::NSUB; ++sb) {
+      if (inner) {
+        tile_glds_fast(buf + sb * SUB, Q + q0 * p.ldq + 64 * sb, go_q, w);
+        tile_glds_fast(buf + (C::NSUB + sb) * SUB, dO + q0 * p.ldo + 64 * sb, go_d, w);
+      } else {
+        tile_glds<SW_DUAL>(buf + sb * SUB, Q + 64 * sb, p.ldq, q0, p.Lq, w, lane);
+        tile_glds<SW_DUAL>(buf + (C::NSUB + sb) * SUB, dO + 64 * sb, p.ldo, q0, p.Lq, w, lane);
+      }
     }
     if (w < 2) {
       const long n = p.Lq - q0;
       const int i = inner ? lane : (lane < n ? lane : (int)n - 1);  // ragged tail: clamp (masked later)
-      glds_f32(buf + 2 * TILE + w * TL * 4, (w == 0 ? LSE : DLT) + q0 + i);
+      glds_f32(buf + 2 * C::NSUB * SUB + w * TL * 4, (w == 0 ? LSE : DLT) + q0 + i);
     }
   };
-  auto wait_next = [&](bool two_in_flight) {  // this wave's share of the older tile has landed
-    if (!two_in_flight)
-      OWLK_VMCNT(0);
+  auto wait_oldest = [&](int younger) {  // this wave's share of the oldest issued tile landed
+    if (younger <= 0)
+      vmcnt<0>();
     else if (w < 2)
-      OWLK_VMCNT(5);
+      vmcnt<C::OPS + 1>();
     else
-      OWLK_VMCNT(4);
+      vmcnt<C::OPS>();
   };
-  if (ntiles > 0) issue(smem, qbeg);
-  if (ntiles > 1) issue(smem + BUF, qbeg + TL);
-  wait_next(ntiles > 1);
+#pragma unroll
+  for (int i = 0; i < C::NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * BUF, qbeg + (long)i * TL);
+  wait_oldest(min(C::NBUF - 2, ntiles - 1));
   OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
     const long q0 = qbeg + (long)t * TL;
-    const bool more2 = t + 2 < ntiles;
-    if (more2) issue(smem + ((t + 2) % 3) * BUF, q0 + 2 * TL);
-    const char* lq = smem + (t % 3) * BUF;
-    const char* ld = lq + TILE;
-    const float* l2 = (const float*)(lq + 2 * TILE);
-    const float* dlt = (const float*)(lq + 2 * TILE + TL * 4);
+    if (t + C::NBUF - 1 < ntiles) issue(smem + ((t + C::NBUF - 1) % C::NBUF) * BUF, q0 + (long)(C::NBUF - 1) * TL);
+    const char* lq = smem + (t % C::NBUF) * BUF;
+    const char* ld = lq + C::NSUB * SUB;
+    const float* l2 = (const float*)(lq + 2 * C::NSUB * SUB);
+    const float* dlt = l2 + TL;
 
     const long qlast = (q0 + TL - 1 < p.Lq ? q0 + TL - 1 : p.Lq - 1);
     int kind = TILE_EMPTY;
@@ -162,9 +176,11 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
       for (int qb = 0; qb < 2; ++qb) {
         f32x16 st = f32x16{}, dp = f32x16{};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq, 32 * qb, s, lane), kf[s], st, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(ld, 32 * qb, s, lane), vf[s], dp, 0, 0, 0);
+        for (int s = 0; s < C::NS; ++s) {
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq + (s >> 2) * SUB, 32 * qb, s & 3, lane),
+                                                       kf[s], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(ld + (s >> 2) * SUB, 32 * qb, s & 3, lane),
+                                                       vf[s], dp, 0, 0, 0);
         }
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -190,30 +206,31 @@ __global__ __launch_bounds__(256, OWLK_DKDV_WAVES) void attn_bwd_dkdv_k(BwdP p) 
         for (int s = 0; s < 2; ++s) {
           const bf16x8 pf = acc_frag(st, s), sf = acc_frag(dp, s);
 #pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(ld, 32 * qb, s, db, lane), pf, dv[db],
-                                                             0, 0, 0);
-            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(lq, 32 * qb, s, db, lane), sf, dk[db],
-                                                             0, 0, 0);
+          for (int db = 0; db < C::NDB; ++db) {
+            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                frag_tr<SW_DUAL>(ld + (db >> 1) * SUB, 32 * qb, s, db & 1, lane), pf, dv[db], 0, 0, 0);
+            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                frag_tr<SW_DUAL>(lq + (db >> 1) * SUB, 32 * qb, s, db & 1, lane), sf, dk[db], 0, 0, 0);
           }
         }
       }
     }
-    wait_next(more2);
+    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));
     OWLK_BARRIER();
   }
 
   if (my_k < p.Lkv) {
-    store_rowT(p.dk + b * p.sdkb + my_k * p.lddk + head * D, dk, p.scale, h);
-    store_rowT(p.dv + b * p.sdvb + my_k * p.lddv + head * D, dv, 1.f, h);
+    store_rowT<C::NDB>(p.dk + b * p.sdkb + my_k * p.lddk + head * D, dk, p.scale, h);
+    store_rowT<C::NDB>(p.dv + b * p.sdvb + my_k * p.lddv + head * D, dv, 1.f, h);
   }
 }
 
 // ======================================================================== dQ
-__global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(BwdP p) {
-  constexpr int TILE = TL * D * 2;
-  constexpr int BUF = 2 * TILE;  // K | V
-  __shared__ __attribute__((aligned(16))) char smem[3 * BUF];
+template <int D>
+__global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
+  using C = Cfg<D>;
+  constexpr int BUF = 2 * C::NSUB * SUB;  // K | V
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF];
   __shared__ int red_lo;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
@@ -251,9 +268,9 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(BwdP p) {
 
   const long my_q = r0 + ql;
   const bool qok = my_q < p.Lq;
-  bf16x8 qf[4], df[4];
+  bf16x8 qf[C::NS], df[C::NS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < C::NS; ++s) {
     qf[s] = qok ? *(const bf16x8*)(Q + my_q * p.ldq + 16 * s + 8 * h) : bf16x8{};
     df[s] = qok ? *(const bf16x8*)(dO + my_q * p.ldo + 16 * s + 8 * h) : bf16x8{};
   }
@@ -262,36 +279,42 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(BwdP p) {
   const bool wave_live = r0 < p.Lq;
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  const int my_fq = frame_of(m, (qok ? my_q : wlast) + m.q_offset);
 
-  f32x16 dq[2];
-  dq[0] = dq[1] = f32x16{};
-  // K / V tiles by LDS-DMA into a 3-deep ring (as in the forward), two tiles in flight
+  f32x16 dq[C::NDB];
+#pragma unroll
+  for (int db = 0; db < C::NDB; ++db) dq[db] = f32x16{};
+
+  // K / V tiles by LDS-DMA into the ring (as in the forward)
   const GldsOff go_k = glds_offsets<SW_DUAL>(p.ldk, w, lane), go_v = glds_offsets<SW_ROW>(p.ldv, w, lane);
   auto issue = [&](char* buf, long c0) {
-    if (c0 + TL <= p.Lkv) {
-      tile_glds_fast(buf, K + c0 * p.ldk, go_k, w);
-      tile_glds_fast(buf + TILE, V + c0 * p.ldv, go_v, w);
-    } else {
-      tile_glds<SW_DUAL>(buf, K, p.ldk, c0, p.Lkv, w, lane);
-      tile_glds<SW_ROW>(buf + TILE, V, p.ldv, c0, p.Lkv, w, lane);
+#pragma unroll
+    for (int sb = 0; sb < C::NSUB; ++sb) {
+      if (c0 + TL <= p.Lkv) {
+        tile_glds_fast(buf + sb * SUB, K + c0 * p.ldk + 64 * sb, go_k, w);
+        tile_glds_fast(buf + (C::NSUB + sb) * SUB, V + c0 * p.ldv + 64 * sb, go_v, w);
+      } else {
+        tile_glds<SW_DUAL>(buf + sb * SUB, K + 64 * sb, p.ldk, c0, p.Lkv, w, lane);
+        tile_glds<SW_ROW>(buf + (C::NSUB + sb) * SUB, V + 64 * sb, p.ldv, c0, p.Lkv, w, lane);
+      }
     }
   };
-  if (ntiles > 0) issue(smem, kv_begin);
-  if (ntiles > 1) {
-    issue(smem + BUF, kv_begin + TL);
-    OWLK_VMCNT(4);
-  } else {
-    OWLK_VMCNT(0);
-  }
+  auto wait_oldest = [&](int younger) {
+    if (younger > 0)
+      vmcnt<C::OPS>();
+    else
+      vmcnt<0>();
+  };
+#pragma unroll
+  for (int i = 0; i < C::NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * BUF, kv_begin + (long)i * TL);
+  wait_oldest(min(C::NBUF - 2, ntiles - 1));
   OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
     const long c0 = kv_begin + (long)t * TL;
-    const bool more2 = t + 2 < ntiles;
-    if (more2) issue(smem + ((t + 2) % 3) * BUF, c0 + 2 * TL);
-    const char* lk = smem + (t % 3) * BUF;
-    const char* lv = lk + TILE;
+    if (t + C::NBUF - 1 < ntiles) issue(smem + ((t + C::NBUF - 1) % C::NBUF) * BUF, c0 + (long)(C::NBUF - 1) * TL);
+    const char* lk = smem + (t % C::NBUF) * BUF;
+    const char* lv = lk + C::NSUB * SUB;
     const long clast = (c0 + TL - 1 < p.Lkv ? c0 + TL - 1 : p.Lkv - 1);
     int kind = TILE_EMPTY;
     if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
@@ -306,9 +329,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(BwdP p) {
       for (int kb = 0; kb < 2; ++kb) {
         f32x16 st = f32x16{}, dp = f32x16{};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lk, 32 * kb, s, lane), qf[s], st, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_ROW>(lv, 32 * kb, s, lane), df[s], dp, 0, 0, 0);
+        for (int s = 0; s < C::NS; ++s) {
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lk + (s >> 2) * SUB, 32 * kb, s & 3, lane),
+                                                       qf[s], st, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_ROW>(lv + (s >> 2) * SUB, 32 * kb, s & 3, lane),
+                                                       df[s], dp, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L2));
@@ -324,19 +349,31 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(BwdP p) {
         for (int s = 0; s < 2; ++s) {
           const bf16x8 sf = acc_frag(dp, s);
 #pragma unroll
-          for (int db = 0; db < 2; ++db)
-            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(lk, 32 * kb, s, db, lane), sf, dq[db],
-                                                             0, 0, 0);
+          for (int db = 0; db < C::NDB; ++db)
+            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                frag_tr<SW_DUAL>(lk + (db >> 1) * SUB, 32 * kb, s, db & 1, lane), sf, dq[db], 0, 0, 0);
         }
       }
     }
-    if (more2)
-      OWLK_VMCNT(4);
-    else
-      OWLK_VMCNT(0);
+    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));
     OWLK_BARRIER();
   }
-  if (qok) store_rowT(p.dq + b * p.sdqb + my_q * p.lddq + head * D, dq, p.scale, h);
+  if (qok) store_rowT<C::NDB>(p.dq + b * p.sdqb + my_q * p.lddq + head * D, dq, p.scale, h);
+}
+
+template <int D>
+int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipStream_t s) {
+  if (phases & 1) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_k<D>, dim3((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B),
+                       dim3(256), 0, s, p);
+    if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
+  }
+  if (phases & 2) {
+    hipLaunchKernelGGL(attn_bwd_dq_k<D>, dim3((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256),
+                       0, s, p);
+    if (int e = owlk::check_launch("attn_bwd_dq")) return e;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -347,7 +384,7 @@ static int attn_bwd_impl(int phases, const void* q, long ldq, long sqb, const vo
                          long lddv, long sdvb, long B, int H, long Lq, long Lkv, int head_dim, float scale, long tpf,
                          int window, int causal, const int* kv_lo, const int* q_hi, const int* run_start,
                          const int* doc, long fstride, void* stream) {
-  OWLK_REQUIRE(head_dim == D, "attn_bwd: head_dim %d not built (64 only)", head_dim);
+  OWLK_REQUIRE(head_dim == 64 || head_dim == 128, "attn_bwd: head_dim %d not built (64, 128)", head_dim);
   OWLK_REQUIRE(tpf > 0 && Lq > 0 && Lkv > 0 && B > 0 && H > 0 && Lq == Lkv, "attn_bwd: training shapes only");
   OWLK_REQUIRE(!doc || run_start, "attn_bwd: doc mask needs run_start");
   OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)dout | (uintptr_t)dq | (uintptr_t)dk |
@@ -364,17 +401,7 @@ static int attn_bwd_impl(int phases, const void* q, long ldq, long sqb, const vo
   p.scale_log2 = scale * LOG2E;
   p.m = owlk_make_mask(tpf, window, causal, 0, Lkv, kv_lo, q_hi, run_start, doc, fstride);
   hipStream_t s = (hipStream_t)stream;
-  if (phases & 1) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256),
-                       0, s, p);
-    if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
-  }
-  if (phases & 2) {
-    hipLaunchKernelGGL(attn_bwd_dq_k, dim3((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256), 0,
-                       s, p);
-    if (int e = owlk::check_launch("attn_bwd_dq")) return e;
-  }
-  return 0;
+  return head_dim == 64 ? launch_bwd<64>(phases, p, B, H, Lq, Lkv, s) : launch_bwd<128>(phases, p, B, H, Lq, Lkv, s);
 }
 
 #define OWLK_BWD_ARGS                                                                                            \

@@ -1,4 +1,4 @@
-// Block-sparse frame-causal flash attention, forward (gfx950, head_dim 64).
+// Block-sparse frame-causal flash attention, forward (gfx950, head_dim 64 and 128).
 //
 // Replaces the compiled flex_attention + create_block_mask pair of the reference
 // (attn.py:13-16, 24-62, 106-109; mmattn.py:75).  Semantics: softmax(q k^T / sqrt(D)) v over the
@@ -9,26 +9,34 @@
 // tile the wave computes S^T = K Q^T with v_mfma_f32_32x32x16_bf16 (key rows in registers, the
 // query on the lane) so the softmax row statistics stay in-lane (+ one lane^32 exchange), then
 // feeds the S^T accumulators straight back as the B operand of O^T += V^T P^T (V^T fragments
-// through ds_read_b64_tr_b16).  K/V tiles arrive by LDS-DMA into a 3-deep ring.
+// through ds_read_b64_tr_b16).  K/V tiles arrive by LDS-DMA into a ring (3 deep at D 64, 2 at D 128).
 // lse is written in base 2 of the scaled logits, lse2 = log2 sum_k exp2(scale log2(e) s_k) (=
 // natural lse * log2 e): the backward's P = exp2(c s - lse2) then needs no conversion.
 #include "attn_common.hpp"
 
-#include <cstdlib>
-#include <type_traits>
 
 namespace {
 
-constexpr int D = 64;
-constexpr int QT = 128;  // query rows per workgroup
-constexpr int KT = 64;   // keys per tile
+constexpr int QT = 128;              // query rows per workgroup (4 waves x 32)
+constexpr int KT = 64;               // keys per tile
+constexpr int SUB = KT * 64 * 2;     // one 64-key x 64-column bf16 sub-tile (128-B rows): 8 KiB
 constexpr float LOG2E = 1.4426950408889634f;
-constexpr float LN2 = 0.6931471805599453f;
+
+// head_dim D is processed as D/64 column sub-tiles of the 64-column layout (same swizzles and
+// fragment readers for every D).  LDS ring depth: 3 tiles at D 64 (48 KiB -> 3 WGs/CU), 2 at
+// D 128 (64 KiB -> 2 WGs/CU).
+template <int D>
+struct Cfg {
+  static constexpr int NSUB = D / 64, NS = D / 16, NDB = D / 32;
+  static constexpr int NBUF = D == 64 ? 3 : 2;
+  static constexpr int TILEB = 2 * NSUB * SUB;  // K sub-tiles | V sub-tiles
+  static constexpr int OPS = 4 * NSUB;          // LDS-DMA wave-instructions per tile per wave
+};
 
 struct FwdP {
   const bf16 *q, *k, *v;
   bf16* o;
-  float* lse;           // [B, H, Lq]
+  float* lse;                   // [B, H, Lq], base 2
   long ldq, ldk, ldv, ldo;      // token row strides (elements)
   long sqb, skb, svb, sob;      // batch strides (elements)
   long Lq, Lkv;
@@ -38,39 +46,21 @@ struct FwdP {
   MaskP m;
 };
 
-// stage one 64x64 bf16 tile (rows r0.., 128-B rows) into registers: 2 chunks per thread
-DEV void stage_load(bf16x8 (&r)[2], const bf16* base, long ld, long r0, long R) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = threadIdx.x + 256 * i;
-    const long row = r0 + (c >> 3);
-    r[i] = row < R ? *(const bf16x8*)(base + row * ld + (c & 7) * 8) : bf16x8{};
-  }
+template <int N>
+DEV void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool TR>
-DEV void stage_store(char* lds, const bf16x8 (&r)[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = threadIdx.x + 256 * i;
-    const int row = c >> 3, ch = c & 7;
-    const int sw = TR ? swz_tr(row) : swz_row(row);
-    *(bf16x8*)(lds + row * 128 + ((ch ^ sw) << 4)) = r[i];
-  }
-}
-
-// GLDS = true: K/V tiles arrive by LDS-DMA into a 3-deep ring with two tiles in flight (no
-// staging registers, counted vmcnt + raw s_barrier); false: register-staged double buffer.
 // BOUNDED = true: the caller guarantees |q.k| <= p.bound (QK-RMSNorm'd q, k have |q| = |k| =
 // sqrt(D), attn.py:84), so every exp2 argument c*s lies in [-c*bound, c*bound] (+-11.8 at D 64):
 // p = exp2(c s) needs no running max, no offset and no rescale.  Softmax is shift-invariant, so
 // the result is the same function; P keeps bf16's relative precision at any magnitude.
-template <bool GLDS, bool BOUNDED>
+template <int D, bool BOUNDED>
 __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
-  constexpr int NBUF = GLDS ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * KT * D * 2];  // [buf][K|V][64][64]
+  using C = Cfg<D>;
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::TILEB];
   __shared__ int red_lo;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const long b = blockIdx.z;
   const int head = blockIdx.y;
@@ -107,16 +97,16 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
 
   // ---- this wave's query fragments (B operand of S^T = K Q^T): Q[row][16s + 8h .. +8]
   const long my_q = r0 + ql;
-  bf16x8 qf[4];
+  bf16x8 qf[C::NS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < C::NS; ++s)
     qf[s] = my_q < p.Lq ? *(const bf16x8*)(Q + my_q * p.ldq + 16 * s + 8 * h) : bf16x8{};
   if constexpr (BOUNDED) {
     // q' = bf16(q * c), c = scale * log2(e): S' = K q'^T is already the exp2 argument.  With
-    // |q.k| <= bound, |S'| <= c * bound (checked < 40 on the host), so p = exp2(S') needs no
-    // running max and no offset; the one extra rounding of q' is 2^-9 relative per element.
+    // |q.k| <= bound, |S'| <= c * bound (checked on the host), so p = exp2(S') needs no running
+    // max and no offset; the one extra rounding of q' is 2^-9 relative per element.
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < C::NS; ++s) {
       float f[8];
       unpack8(qf[s], f);
 #pragma unroll
@@ -127,61 +117,46 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const bool wave_live = r0 < p.Lq;
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  const int my_fq = frame_of(m, (my_q < p.Lq ? my_q : wlast) + m.q_offset);
 
-  f32x16 o[2];
-  o[0] = f32x16{};
-  o[1] = f32x16{};
+  f32x16 o[C::NDB];
+#pragma unroll
+  for (int db = 0; db < C::NDB; ++db) o[db] = f32x16{};
   float mrow = BOUNDED ? 0.f : -INFINITY, lrow = 0.f;
 
-  constexpr int BUFB = 2 * KT * D * 2;
-  bf16x8 kr[2], vr[2];
+  // ---- K / V tiles by LDS-DMA into a C::NBUF-deep ring, C::NBUF - 1 tiles in flight; per-lane
+  // source offsets hoisted (wave-uniform tile bases), per-lane clamping only on the ragged tail
   const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_TR>(p.ldv, w, lane);
-  if (GLDS) {
-    if (ntiles > 0) {
-      tile_glds<SW_ROW>(smem, K, p.ldk, kv_begin, p.Lkv, w, lane);
-      tile_glds<SW_TR>(smem + KT * D * 2, V, p.ldv, kv_begin, p.Lkv, w, lane);
+  auto issue = [&](char* buf, long c0) {
+#pragma unroll
+    for (int sb = 0; sb < C::NSUB; ++sb) {
+      if (c0 + KT <= p.Lkv) {
+        tile_glds_fast(buf + sb * SUB, K + c0 * p.ldk + 64 * sb, goff_k, w);
+        tile_glds_fast(buf + (C::NSUB + sb) * SUB, V + c0 * p.ldv + 64 * sb, goff_v, w);
+      } else {
+        tile_glds<SW_ROW>(buf + sb * SUB, K + 64 * sb, p.ldk, c0, p.Lkv, w, lane);
+        tile_glds<SW_TR>(buf + (C::NSUB + sb) * SUB, V + 64 * sb, p.ldv, c0, p.Lkv, w, lane);
+      }
     }
-    if (ntiles > 1) {
-      tile_glds<SW_ROW>(smem + BUFB, K, p.ldk, kv_begin + KT, p.Lkv, w, lane);
-      tile_glds<SW_TR>(smem + BUFB + KT * D * 2, V, p.ldv, kv_begin + KT, p.Lkv, w, lane);
-      OWLK_VMCNT(4);
-    } else {
-      OWLK_VMCNT(0);
-    }
-    OWLK_BARRIER();
-  } else {
-    if (ntiles > 0) {
-      stage_load(kr, K, p.ldk, kv_begin, p.Lkv);
-      stage_load(vr, V, p.ldv, kv_begin, p.Lkv);
-      stage_store<false>(smem, kr);
-      stage_store<true>(smem + KT * D * 2, vr);
-    }
-    __syncthreads();
-  }
+  };
+  // wait until the oldest issued tile has landed, `younger` more tiles may stay in flight
+  auto wait_oldest = [&](int younger) {
+    if (younger > 0)
+      vmcnt<C::OPS>();
+    else
+      vmcnt<0>();
+  };
+#pragma unroll
+  for (int i = 0; i < C::NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * C::TILEB, kv_begin + (long)i * KT);
+  wait_oldest(min(C::NBUF - 2, ntiles - 1));
+  OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
     const long c0 = kv_begin + (long)t * KT;
-    const bool more = t + 1 < ntiles;
-    const bool more2 = t + 2 < ntiles;
-    if (GLDS) {
-      if (more2) {
-        char* nb = smem + ((t + 2) % 3) * BUFB;
-        const long c2 = c0 + 2 * KT;
-        if (c2 + KT <= p.Lkv) {
-          tile_glds_fast(nb, K + c2 * p.ldk, goff_k, w);
-          tile_glds_fast(nb + KT * D * 2, V + c2 * p.ldv, goff_v, w);
-        } else {
-          tile_glds<SW_ROW>(nb, K, p.ldk, c2, p.Lkv, w, lane);
-          tile_glds<SW_TR>(nb + KT * D * 2, V, p.ldv, c2, p.Lkv, w, lane);
-        }
-      }
-    } else if (more) {
-      stage_load(kr, K, p.ldk, c0 + KT, p.Lkv);
-      stage_load(vr, V, p.ldv, c0 + KT, p.Lkv);
-    }
-    const char* lk = smem + (GLDS ? (t % 3) : (t & 1)) * BUFB;
-    const char* lv = lk + KT * D * 2;
+    if (t + C::NBUF - 1 < ntiles)
+      issue(smem + ((t + C::NBUF - 1) % C::NBUF) * C::TILEB, c0 + (long)(C::NBUF - 1) * KT);
+    const char* lk = smem + (t % C::NBUF) * C::TILEB;
+    const char* lv = lk + C::NSUB * SUB;
 
     const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
     int kind = TILE_EMPTY;
@@ -198,8 +173,9 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
         st[kb] = f32x16{};
         const int krow = 32 * kb + ql;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bf16x8 kf = *(const bf16x8*)(lk + krow * 128 + (((2 * s + h) ^ swz_row(krow)) << 4));
+        for (int s = 0; s < C::NS; ++s) {
+          const bf16x8 kf = *(const bf16x8*)(lk + (s >> 2) * SUB + krow * 128 +
+                                             (((2 * (s & 3) + h) ^ swz_row(krow)) << 4));
           st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[kb], 0, 0, 0);
         }
       }
@@ -223,7 +199,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
           const float alpha = __builtin_amdgcn_exp2f(mrow * p.scale_log2 - mc);
           lrow *= alpha;
 #pragma unroll
-          for (int db = 0; db < 2; ++db)
+          for (int db = 0; db < C::NDB; ++db)
 #pragma unroll
             for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
         }
@@ -248,34 +224,22 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
         for (int s = 0; s < 2; ++s) {
           const bf16x8 pf = acc_frag(st[kb], s);
 #pragma unroll
-          for (int db = 0; db < 2; ++db)
-            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_TR>(lv, 32 * kb, s, db, lane), pf, o[db], 0, 0,
-                                                            0);
+          for (int db = 0; db < C::NDB; ++db)
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                frag_tr<SW_TR>(lv + (db >> 1) * SUB, 32 * kb, s, db & 1, lane), pf, o[db], 0, 0, 0);
         }
     }
-    if (GLDS) {
-      if (more2)
-        OWLK_VMCNT(4);  // tile t+1 landed (this wave's part); t+2 may stay in flight
-      else
-        OWLK_VMCNT(0);
-      OWLK_BARRIER();
-    } else {
-      if (more) {
-        char* nb = smem + ((t + 1) & 1) * BUFB;
-        stage_store<false>(nb, kr);
-        stage_store<true>(nb + KT * D * 2, vr);
-      }
-      __syncthreads();
-    }
+    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));  // tile t+1 landed (this wave's part)
+    OWLK_BARRIER();
   }
 
-  // ---- epilogue: O = O^T / l, lse
+  // ---- epilogue: O = O^T / l, lse2
   const float ltot = lrow + __shfl_xor(lrow, 32, 64);
   if (my_q < p.Lq) {
     const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
     bf16* O = p.o + b * p.sob + my_q * p.ldo + head * D;
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+    for (int db = 0; db < C::NDB; ++db)
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         bf16x4 v4;
@@ -286,6 +250,14 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
     if (h == 0)
       p.lse[(b * p.H + head) * p.Lq + my_q] = ltot > 0.f ? mrow * p.scale_log2 + __log2f(ltot) : -INFINITY;
   }
+}
+
+template <int D>
+void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
+  if (p.bound > 0.f)
+    hipLaunchKernelGGL((attn_fwd_k<D, true>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((attn_fwd_k<D, false>), grid, dim3(256), 0, s, p);
 }
 
 }  // namespace
@@ -312,7 +284,7 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
                              long Lkv, int head_dim, float scale, float score_bound, long tpf, int window,
                              int causal, long q_offset, const int* kv_lo, const int* q_hi, const int* run_start,
                              const int* doc, long fstride, void* stream) {
-  OWLK_REQUIRE(head_dim == D, "attn_fwd: head_dim %d not built (64 only)", head_dim);
+  OWLK_REQUIRE(head_dim == 64 || head_dim == 128, "attn_fwd: head_dim %d not built (64, 128)", head_dim);
   OWLK_REQUIRE(tpf > 0 && Lq > 0 && Lkv > 0 && B > 0 && H > 0, "attn_fwd: bad sizes");
   OWLK_REQUIRE((Lkv + q_offset) < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_fwd: sequence too long");
   OWLK_REQUIRE(!doc || (run_start != nullptr), "attn_fwd: doc mask needs run_start");
@@ -329,15 +301,9 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
   OWLK_REQUIRE(score_bound >= 0.f && score_bound * scale < 40.f, "attn_fwd: score_bound out of range");
   p.m = owlk_make_mask(tpf, window, causal, q_offset, Lkv, kv_lo, q_hi, run_start, doc, fstride);
   dim3 grid((unsigned)((Lq + QT - 1) / QT), (unsigned)H, (unsigned)B);
-  static const int variant = getenv("OWLK_ATTN_FWD_REGSTAGE") ? 0 : 1;
-  const bool bounded = score_bound > 0.f;
-  if (variant && bounded)
-    hipLaunchKernelGGL((attn_fwd_k<true, true>), grid, dim3(256), 0, (hipStream_t)stream, p);
-  else if (variant)
-    hipLaunchKernelGGL((attn_fwd_k<true, false>), grid, dim3(256), 0, (hipStream_t)stream, p);
-  else if (bounded)
-    hipLaunchKernelGGL((attn_fwd_k<false, true>), grid, dim3(256), 0, (hipStream_t)stream, p);
+  if (head_dim == 64)
+    launch_fwd<64>(p, grid, (hipStream_t)stream);
   else
-    hipLaunchKernelGGL((attn_fwd_k<false, false>), grid, dim3(256), 0, (hipStream_t)stream, p);
+    launch_fwd<128>(p, grid, (hipStream_t)stream);
   return owlk::check_launch("attn_fwd");
 }

@@ -45,11 +45,14 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"libowlk.so not built at {LIB_PATH}: run `make -C owl-audio-exps_amd/csrc` "
+        path = os.environ.get("OWLK_LIB", LIB_PATH)  # A/B builds (tools/); default: the in-tree library
+        if not os.path.exists(path):
+            raise RuntimeError(f"libowlk.so not built at {path}: run `make -C owl-audio-exps_amd/csrc` "
                                "(or __graft_entry__.build()); there is no non-HIP fallback")
-        h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        h = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, args in _SIGS.items():
+            if path != LIB_PATH and not hasattr(h, name):  # older A/B build: symbol not there
+                continue
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int

@@ -6,6 +6,7 @@ Both counters are in KiB."""
 import csv
 import glob
 import json
+import re
 import sys
 from collections import defaultdict
 
@@ -13,7 +14,8 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob("gpurun_out/traffic/*_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0].split("::")[-1].split("<")[0]
+        mt = re.search(r"::(\w+?)_k\b", r["Kernel_Name"])  # attn_bwd_dkdv_k<64>(...) -> attn_bwd_dkdv
+        name = mt.group(1) if mt else r["Kernel_Name"][:60]
         vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]) * 1024)
 out = {}
 for k, d in vals.items():
