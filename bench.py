@@ -28,7 +28,24 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "latent-tokens/sec/GPU (fwd+bwd) DiT-v4 bf16; 1/2/4/8-GPU scaling"
 PEAK_BF16 = 2.5e15           # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: Peak BF16 MFMA)
 PEAK_HBM = 8.0e12
-FLOP_PER_TOKEN = 6.596e9     # dit_v4 fwd+bwd algorithmic FLOPs per token
+FLOP_PER_TOKEN = 6.596e9     # dit_v4 fwd+bwd algorithmic FLOPs per token; see flops_per_token
+
+
+def flops_per_token(mc, tokens):
+    """SURVEY §8(d) counting for any DiT config: 3 x (token GEMMs 24 d^2 per layer + attention 4 d x
+    allowed pairs / T + proj_in/out + per-frame modulation/embedding GEMMs / tpf) -- fwd+bwd, no
+    recompute, no masked pairs.  Gives 6.601e9 for dit_v4 and 3.161e10 for dit_v4_5B (SURVEY:
+    6.596e9 / 3.158e10); the headline line keeps SURVEY's dit_v4 figure."""
+    from owl_wms import kernels as K
+    d, L, tpf = mc.d_model, mc.n_layers, mc.tokens_per_frame
+    gemm = 24 * d * d * L + 2 * 2 * mc.channels * d
+    per_frame = (4 * 2 * 2 * d * d * L + 2 * 2 * 2 * d * d) / tpf  # 4 mod fcs/layer + final AdaLN fc
+    attn = 0.0
+    for i in range(L):
+        local = i % 4 != 0
+        w = mc.local_window if local else getattr(mc, "global_window", None)
+        attn += 4 * d * K.mask_pairs(K.FrameMask(tpf, w), tokens, tokens) / tokens
+    return 3 * (gemm + per_frame + attn)
 
 
 def log(*a):
@@ -79,6 +96,8 @@ def main():
     ap.add_argument("--frames", type=int, default=1536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--config", default="configs/dit_v4.yml",
+                    help="model config; the headline metric is dit_v4 (others, e.g. dit_v4_5B, report their own line)")
     args = ap.parse_args()
 
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
@@ -95,13 +114,17 @@ def main():
     from owl_wms.muon import init_muon
     from owl_wms.utils.grad_reducer import EMA, GradReducer
 
-    cfg = Config.from_yaml(os.path.join(REPO, "configs", "dit_v4.yml"))
+    cfg = Config.from_yaml(os.path.join(REPO, args.config))
+    cfg_name = os.path.splitext(os.path.basename(args.config))[0]
+    headline = cfg_name == "dit_v4"
     mc = cfg.model
     mc.n_frames = args.frames
     tokens = mc.n_frames * mc.tokens_per_frame
     accum = max(1, args.global_batch // world)
     torch.manual_seed(0)
     model = get_model_cls(mc.model_id)(mc).cuda().train()
+    fpt = flops_per_token(mc, tokens)
+    n_params = sum(p.numel() for p in model.parameters())
     if world > 1:
         with torch.no_grad():
             for p in model.parameters():
@@ -194,21 +217,23 @@ def main():
             log(f"  total kernel time {tot_ms:.1f} ms")
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         cpu = cpu_baseline()
 
     if rank == 0:
-        out = {"metric": METRIC, "value": round(value, 1), "unit": "latent-tokens/s", "n_gpus": world,
+        metric = METRIC if headline else f"latent-tokens/sec/GPU (fwd+bwd) {cfg_name} bf16"
+        out = {"metric": metric, "value": round(value, 1), "unit": "latent-tokens/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 1),
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
-               "data": "synthetic (random latents of the dit_v4 shape, random-init weights)",
-               "config": {"workload": f"configs/dit_v4.yml training step: global batch {args.global_batch} x "
+               "data": f"synthetic (random latents of the {cfg_name} shape, random-init weights)",
+               "config": {"workload": f"{args.config} training step: global batch {args.global_batch} x "
                                       f"{mc.n_frames} frames x 8x8 latents ({tokens} tokens/sample), fwd+bwd + "
                                       f"RCCL grad all-reduce + Muon/AdamW step + EMA",
-                          "model": "dit_v4 (16 L, d1536, 24 H, 704.9M params)", "global_batch": args.global_batch,
+                          "model": f"{cfg_name} ({mc.n_layers} L, d{mc.d_model}, {mc.n_heads} H, "
+                                   f"{n_params / 1e6:.1f}M params)", "global_batch": args.global_batch,
                           "seq_len": tokens, "parallelism": f"dp{world}"},
                "tokens_per_s_per_gpu": round(value / world, 1),
-               "step_mfma_frac": round(value * FLOP_PER_TOKEN / world / PEAK_BF16, 4),
+               "step_mfma_frac": round(value * (FLOP_PER_TOKEN if headline else fpt) / world / PEAK_BF16, 4),
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:

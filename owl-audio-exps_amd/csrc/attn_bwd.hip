@@ -68,9 +68,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   __shared__ int red_hi;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const long b = blockIdx.z;
-  const int head = blockIdx.y;
-  const long k0 = (long)blockIdx.x * TB;
+  const BlockIds bid = xcd_block_ids();
+  const long b = bid.z;
+  const int head = bid.y;
+  const long k0 = (long)bid.x * TB;
   const long kw0 = k0 + 32 * w;
   const MaskP& m = p.m;
 
@@ -234,10 +235,11 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
   __shared__ int red_lo;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const long b = blockIdx.z;
-  const int head = blockIdx.y;
+  const BlockIds bid = xcd_block_ids();
+  const long b = bid.z;
+  const int head = bid.y;
   const int ntq = (int)((p.Lq + TB - 1) / TB);
-  const long q0 = (long)(ntq - 1 - (int)blockIdx.x) * TB;
+  const long q0 = (long)(ntq - 1 - bid.x) * TB;
   const long r0 = q0 + 32 * w;
   const MaskP& m = p.m;
 

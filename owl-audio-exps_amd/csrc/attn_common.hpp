@@ -216,6 +216,27 @@ DEV void glds_f32(char* lds_row, const float* src) {
                                    (void __attribute__((address_space(3)))*)lds_row, 4, 0, 0);
 }
 
+// XCD-aware workgroup order (cdna_hip_programming.md T1): consecutive workgroups are dealt to
+// the 8 XCDs round-robin, so remap the linear id so that XCD x runs a CONTIGUOUS range of
+// (block, head, batch) triples.  Co-resident workgroups on one XCD then hold neighbouring blocks
+// of the same head and sweep the same Q/dO or K/V tiles a few tiles apart -- L2 (4 MiB/XCD) hits
+// instead of re-fetches.  Bijective (the tail beyond a multiple of 8 keeps its id).
+struct BlockIds {
+  int x, y, z;
+};
+DEV BlockIds xcd_block_ids() {
+  const unsigned nx = gridDim.x, ny = gridDim.y, n = nx * ny * gridDim.z;
+  unsigned lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const unsigned per = n / 8;
+  if (lin < per * 8) lin = (lin % 8) * per + lin / 8;
+  BlockIds r;
+  r.x = (int)(lin % nx);
+  lin /= nx;
+  r.y = (int)(lin % ny);
+  r.z = (int)(lin / ny);
+  return r;
+}
+
 #define OWLK_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #define OWLK_BARRIER() asm volatile("s_barrier" ::: "memory")
 

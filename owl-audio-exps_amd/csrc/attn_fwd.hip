@@ -62,10 +62,11 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   __shared__ int red_lo;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
-  const long b = blockIdx.z;
-  const int head = blockIdx.y;
+  const BlockIds bid = xcd_block_ids();
+  const long b = bid.z;
+  const int head = bid.y;
   const int ntq = (int)((p.Lq + QT - 1) / QT);
-  const long q0 = (long)(ntq - 1 - (int)blockIdx.x) * QT;  // heaviest (latest) query tiles first
+  const long q0 = (long)(ntq - 1 - bid.x) * QT;  // heaviest (latest) query tiles first
   const long r0 = q0 + 32 * w;                             // this wave's first row
   const MaskP& m = p.m;
 

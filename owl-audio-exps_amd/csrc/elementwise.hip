@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R,
   if (col >= N) return;
   const long r0 = (long)blockIdx.y * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (long r = r0; r < r1; ++r) {
+  auto add_row = [&](long r) {
     if constexpr (sizeof(T) == 2) {
       float v[8];
       unpack8(*(const bf16x8*)(x + r * ld + col), v);
@@ -399,7 +399,14 @@ __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R,
         acc[e + 4] += b[e];
       }
     }
+  };
+  long r = r0;
+  // four rows per iteration: four independent 16-B loads in flight per lane (latency-bound otherwise)
+  for (; r + 4 <= r1; r += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add_row(r + u);
   }
+  for (; r < r1; ++r) add_row(r);
 #pragma unroll
   for (int e = 0; e < 8; ++e) atomicAdd(out + col + e, acc[e]);
 }

@@ -346,13 +346,20 @@ DEV void glds_tile(char* lds, const bf16* base, long ld, long r0, long k0, long 
   }
 }
 
-template <bool AT, bool BT, int EPI, bool OF32>
+// BN 256: waves 2 (M) x 4 (N) of 128 x 64, 2-stage ring (128 KiB), the next K-tile's DMA drained
+//         at every K-step (one tile in flight, inside the step).
+// BN 128: waves 4 x 2 of 64 x 64, 3-stage ring (3 x 48 KiB): two K-tiles in flight across the
+//         raw barrier behind a counted vmcnt (cdna_hip_programming.md "Pipelining across
+//         barriers"): the wait at the end of step k retires tile k+1 only.
+template <int BN, bool AT, bool BT, int EPI, bool OF32>
 __global__ __launch_bounds__(NT8, 1) void gemm256_kernel(GemmP p) {
-  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64, TM = 8, TN = 4;
+  constexpr int BM = 256, WARPS_N = BN / 64, WTM = BM / (8 / WARPS_N), WTN = 64, TM = WTM / 16, TN = 4;
+  constexpr int NBUF = BN == 256 ? 2 : 3;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];  // 128 KiB
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  constexpr int OPS = (BM + BN) * BK * 2 / (NT8 * 16);  // LDS-DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STAGE];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WARPS_N, wn = wave % WARPS_N;
 
   const int nwg = p.tiles_m * p.tiles_n;
   int bid = blockIdx.x;
@@ -375,19 +382,26 @@ __global__ __launch_bounds__(NT8, 1) void gemm256_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  glds_tile<BM, AT>(smem, A, p.lda, m0, kbeg, p.M, wave, lane);
-  glds_tile<BN, BT>(smem + A_BYTES, B, p.ldb, n0, kbeg, p.N, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  auto issue = [&](int kt) {
+    char* buf = smem + (kt % NBUF) * STAGE;
+    glds_tile<BM, AT>(buf, A, p.lda, m0, kbeg + (long)kt * BK, p.M, wave, lane);
+    glds_tile<BN, BT>(buf + A_BYTES, B, p.ldb, n0, kbeg + (long)kt * BK, p.N, wave, lane);
+  };
+  auto wait_next = [&](bool younger_in_flight) {
+    if (NBUF > 2 && younger_in_flight)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < nk) issue(i);
+  wait_next(nk > 1);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      char* nb = smem + (cur ^ 1) * STAGE;
-      glds_tile<BM, AT>(nb, A, p.lda, m0, kbeg + (long)(kt + 1) * BK, p.M, wave, lane);
-      glds_tile<BN, BT>(nb + A_BYTES, B, p.ldb, n0, kbeg + (long)(kt + 1) * BK, p.N, wave, lane);
-    }
-    const char* la = smem + cur * STAGE;
+    if (kt + NBUF - 1 < nk) issue(kt + NBUF - 1);
+    const char* la = smem + (kt % NBUF) * STAGE;
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -404,8 +418,8 @@ __global__ __launch_bounds__(NT8, 1) void gemm256_kernel(GemmP p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    wait_next(kt + NBUF - 1 < nk);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
   // ---- epilogue per wave through a private 16 x 64 fp32 LDS strip (reuses the staging ring)
@@ -483,11 +497,16 @@ int dispatch_e(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStrea
 
 template <bool AT, bool BT, int EPI, bool OF32>
 int launch256(GemmP& p, long batch, hipStream_t s) {
+  static const int bn = getenv("OWLK_GEMM_BN") ? atoi(getenv("OWLK_GEMM_BN")) : 256;
+  const bool n128 = bn == 128 && (!BT || p.N % 128 == 0);
   p.tiles_m = (int)((p.M + 255) / 256);
-  p.tiles_n = (int)((p.N + 255) / 256);
+  p.tiles_n = (int)((p.N + (n128 ? 127 : 255)) / (n128 ? 128 : 256));
   const int splits = (int)((p.K + p.kchunk - 1) / p.kchunk);
   dim3 grid(p.tiles_m * p.tiles_n, (unsigned)splits, (unsigned)batch);
-  hipLaunchKernelGGL((gemm256_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  if (n128)
+    hipLaunchKernelGGL((gemm256_kernel<128, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<256, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   return owlk::check_launch("gemm256");
 }
 
