@@ -529,9 +529,11 @@ extern "C" int owlk_mse(const void* pred, const void* tgt, long n, float gscale,
 extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream) {
   OWLK_REQUIRE(N % 8 == 0 && ld % 8 == 0, "colsum: N, ld must be multiples of 8");
   const long cols_blocks = (N / 8 + 255) / 256;
-  long splits = 1024 / cols_blocks;
+  // enough row splits to fill the chip (~2k workgroups), but >= 16 rows per workgroup: every split
+  // adds N atomics onto the same N outputs, and short splits turn into same-address contention
+  long splits = 2048 / cols_blocks;
+  if (splits > R / 16) splits = R / 16;
   if (splits < 1) splits = 1;
-  if (splits > R) splits = R;
   const long rows_per = (R + splits - 1) / splits;
   dim3 g((unsigned)cols_blocks, (unsigned)((R + rows_per - 1) / rows_per));
   if (x_f32)
