@@ -531,6 +531,27 @@ int dispatch256(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStre
   owlk::set_error("gemm: unknown epilogue %d", epi);
   return 1;
 }
+// split-K factor for long reductions onto few 256^2 tiles (weight gradients, K = tokens): at one
+// workgroup per CU (128 KiB LDS) the grid runs in ceil(tiles * s / 256) rounds, so pick s to fill
+// the last round (e.g. 144 tiles: s = 4 -> 2.25 rounds, 75 % of the third idle; s = 7 -> 3.94);
+// >= 2 rounds of work, chunks >= 2048 deep, and a small preference for fewer splits (each adds
+// an fp32 atomic pass over the output).
+long pick_splits(long tiles, long K) {
+  constexpr long CUS = 256;
+  long best = 1;
+  double best_score = -1.0;
+  for (long sp = 2; sp <= 64 && K / sp >= 2048; ++sp) {
+    const long wg = tiles * sp;
+    if (wg < 2 * CUS) continue;
+    const long rounds = (wg + CUS - 1) / CUS;
+    const double score = (double)wg / (double)(rounds * CUS) - 0.004 * (double)sp;
+    if (score > best_score) {
+      best_score = score;
+      best = sp;
+    }
+  }
+  return best;
+}
 }  // namespace
 
 extern "C" int owlk_gemm(long M, long N, long K, long batch,
@@ -569,8 +590,7 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
                        (!b_trans || N % 256 == 0) && !(c_f32 && beta != 0.f && beta != 1.f);
   if (fits256) {
     if (c_f32 && epi == EPI_STORE && beta == 1.f && K >= 8192 && tiles256 < 1024) {
-      long splits = (512 + tiles256 - 1) / tiles256;
-      if (splits > K / 4096) splits = K / 4096;
+      const long splits = pick_splits(tiles256, K);
       if (splits > 1) {
         p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
         return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
