@@ -497,16 +497,11 @@ int dispatch_e(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStrea
 
 template <bool AT, bool BT, int EPI, bool OF32>
 int launch256(GemmP& p, long batch, hipStream_t s) {
-  static const int bn = getenv("OWLK_GEMM_BN") ? atoi(getenv("OWLK_GEMM_BN")) : 256;
-  const bool n128 = bn == 128 && (!BT || p.N % 128 == 0);
   p.tiles_m = (int)((p.M + 255) / 256);
-  p.tiles_n = (int)((p.N + (n128 ? 127 : 255)) / (n128 ? 128 : 256));
+  p.tiles_n = (int)((p.N + 255) / 256);
   const int splits = (int)((p.K + p.kchunk - 1) / p.kchunk);
   dim3 grid(p.tiles_m * p.tiles_n, (unsigned)splits, (unsigned)batch);
-  if (n128)
-    hipLaunchKernelGGL((gemm256_kernel<128, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
-  else
-    hipLaunchKernelGGL((gemm256_kernel<256, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  hipLaunchKernelGGL((gemm256_kernel<256, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   return owlk::check_launch("gemm256");
 }
 

@@ -7,5 +7,5 @@ for i in 1 2 3; do
     2) C="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC";;
     3) C="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F SQ_ACTIVE_INST_VMEM SQ_CYCLES GRBM_GUI_ACTIVE";;
   esac
-  timeout -k 10 240 rocprofv3 --pmc $C --kernel-trace -d $R/gpurun_out/pmc_${WHICH:-fwd} -f csv -o p$i -- python3 $R/tools/attn_fwd_only.py ${WHICH:-fwd} > $R/gpurun_out/pmc_${WHICH:-fwd}_$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $C --kernel-trace -d $R/gpurun_out/pmc_${WHICH:-fwd} -f csv -o p$i -- python3 $R/tools/${PROG:-attn_fwd_only.py} ${WHICH:-fwd} > $R/gpurun_out/pmc_${WHICH:-fwd}_$i.log 2>&1
 done
