@@ -93,7 +93,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-batch", type=int, default=16)
-    ap.add_argument("--frames", type=int, default=1536)
+    ap.add_argument("--frames", type=int, default=None, help="override n_frames (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--config", default="configs/dit_v4.yml",
@@ -118,8 +118,10 @@ def main():
     cfg_name = os.path.splitext(os.path.basename(args.config))[0]
     headline = cfg_name == "dit_v4"
     mc = cfg.model
-    mc.n_frames = args.frames
-    tokens = mc.n_frames * mc.tokens_per_frame
+    if args.frames:
+        mc.n_frames = args.frames
+    tokens = mc.n_frames * mc.tokens_per_frame  # joint video + audio tokens for game_rft_audio
+    av = mc.model_id == "game_rft_audio"
     accum = max(1, args.global_batch // world)
     torch.manual_seed(0)
     model = get_model_cls(mc.model_id)(mc).cuda().train()
@@ -132,13 +134,22 @@ def main():
     opt = init_muon(model, rank=rank, world_size=world, **cfg.train.opt_kwargs)
     ema = EMA(model, beta=0.999)
     red = GradReducer(model.parameters(), world_size=world)
-    batches = [[t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234 + rank * 97 + i)] for i in range(2)]
+    batches = []
+    for i in range(2):
+        b = [t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234 + rank * 97 + i)]
+        if av:
+            g = torch.Generator().manual_seed(4321 + rank * 97 + i)
+            b.append(torch.randn(1, mc.n_frames, mc.audio_channels, generator=g).to(torch.bfloat16).cuda())
+        batches.append(b)
     vae_scale = cfg.train.vae_scale
 
     def micro(i, sync):
-        vid, mouse, btn, doc = batches[i % 2]
+        vid, mouse, btn, doc = batches[i % 2][:4]
         red.begin(sync)
-        loss = model(vid / vae_scale, mouse, btn, doc) / accum
+        if av:
+            loss = model(vid / vae_scale, batches[i % 2][4], mouse, btn)[0] / accum
+        else:
+            loss = model(vid / vae_scale, mouse, btn, doc) / accum
         loss.backward()
         red.finish()
         return loss

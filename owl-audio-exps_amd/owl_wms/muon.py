@@ -26,6 +26,11 @@ def newton_schulz_bf16(G: Tensor, steps: int = 5) -> Tensor:
     assert G.dim() == 3
     b, r, c = G.shape
     tr = r > c
+    # the GEMMs need dims that are multiples of 8: zero-pad (exact -- zero rows/columns add nothing
+    # to ||X||_F or X X^T and stay zero through every iteration), e.g. mouse angle_proj [256, 2]
+    pr, pc = (-r) % 8, (-c) % 8
+    if pr or pc:
+        G = torch.nn.functional.pad(G, (0, pc, 0, pr))
     X = K.ns_normalize(G, tr)
     m = X.shape[1]
     A = torch.empty(b, m, m, device=G.device, dtype=torch.bfloat16)
@@ -36,7 +41,8 @@ def newton_schulz_bf16(G: Tensor, steps: int = 5) -> Tensor:
         K.bgemm(A, A, Bm, epi=K.EPI_AXPBY, alpha=NS_C, beta=NS_B, aux=A)      # B = b A + c A A
         K.bgemm(Bm, X, X2, b_trans=True, epi=K.EPI_AXPBY, alpha=1.0, beta=NS_A, aux=X)  # X = a X + B X
         X, X2 = X2, X
-    return X.transpose(1, 2) if tr else X
+    X = X.transpose(1, 2) if tr else X
+    return X[:, :r, :c] if (pr or pc) else X
 
 
 def zeropower_via_newtonschulz5(G: Tensor, steps: int) -> Tensor:

@@ -307,3 +307,14 @@ def test_layernorm_fwd_bwd(T, d):
     dy = rnd(T, d, seed=73)
     yr.backward(dy.float().cpu())
     assert rel(k.layernorm_bwd(dy, x, mean, rstd), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(256, 2), (3, 40), (12, 13)])
+def test_newton_schulz_padded_shapes(shape):
+    """Shapes whose dims are not multiples of 8 (mmdit_v2 puts control_embed.mouse.angle_proj
+    [256, 2] under Muon) are zero-padded: same result as the oracle NS in the kernel's order."""
+    from owl_wms.muon import newton_schulz_bf16
+    g = torch.randn(*shape, generator=torch.Generator().manual_seed(80))
+    y = newton_schulz_bf16(g[None].to(DEV))[0]
+    ref = R.newton_schulz5(g, 5, order="epilogue")
+    assert y.shape == shape and rel(y, ref) < 2e-2
