@@ -1,0 +1,11 @@
+# One GPU call: GPU parity tests, smoke, bench (N=1 defaults), rocprofv3 kernel-trace stats of the bench.
+# Usage (on the box):  bash tools/round_check.sh TAG
+set -e
+TAG=${1:-r}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/${TAG}_gputests.log 2>&1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1
+timeout -k 10 400 python -u bench.py > $O/${TAG}_bench.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/${TAG}_profbench.log 2>&1
+find $O/${TAG}_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/${TAG}_kernel_stats.csv
