@@ -461,6 +461,175 @@ __global__ __launch_bounds__(NT8, 1) void gemm256_kernel(GemmP p) {
   }
 }
 
+// ======================================================================== 256 x 256, ping-pong
+// Same tile / waves / LDS-DMA staging as gemm256_kernel, scheduled as 4 phases per K-tile with
+// the two wave groups (wr = 0: rows 0-127, wr = 1: rows 128-255 of the tile) one barrier apart
+// (cdna_hip_programming.md §5 "256² 8-phase template", T3-T5): while one wave of a SIMD runs its
+// 16-MFMA quadrant, the other issues the LDS reads and LDS-DMA of its next phase.
+//
+// The ring holds two K-tiles of four 16-KiB half-tiles (A rows 0-127 | A rows 128-255 | B cols
+// 0-127 | B cols 128-255); a wave reads only A half wr and B half wc >> 1.  Per K-tile t
+// (stage t & 1), per wave, quadrants (m half of the wave's 128 rows, n half of its 64 columns):
+//   phase 0: ds_read A(m0) + B(n0) of t; LDS-DMA A(t+1)          MFMA (m0, n0)
+//   phase 1: ds_read B(n1)                                        MFMA (m0, n1)
+//   phase 2: ds_read A(m1)                                        MFMA (m1, n1)
+//   phase 3: LDS-DMA B(t+2); vmcnt -> all of t+1 landed           MFMA (m1, n0)
+// WAR: a half-tile is re-staged only after the barrier that follows the last wave's lgkmcnt on
+// its previous contents (B last read in phase 1, A in phase 2, group 1 one barrier later).
+// RAW: every wave's vmcnt for tile t+1 precedes (in barrier order) the first read of it.
+template <bool AT, bool BT, int EPI, bool OF32>
+__global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
+  constexpr int HALF = 128 * BK * 2, STAGE = 4 * HALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  const long m0 = (long)tm * 256, n0 = (long)tn * 256;
+  const long z = blockIdx.z;
+  const bf16* A = p.A + z * p.sA;
+  const bf16* B = p.B + z * p.sB;
+  const long kbeg = (long)blockIdx.y * p.kchunk;
+  const long kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nk = (int)((kend - kbeg) / BK);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issueA = [&](int t) {
+    char* st = smem + (t & 1) * STAGE;
+    glds_tile<128, AT>(st, A, p.lda, m0, kbeg + (long)t * BK, p.M, wave, lane);
+    glds_tile<128, AT>(st + HALF, A, p.lda, m0 + 128, kbeg + (long)t * BK, p.M, wave, lane);
+  };
+  auto issueB = [&](int t) {
+    char* st = smem + (t & 1) * STAGE + 2 * HALF;
+    glds_tile<128, BT>(st, B, p.ldb, n0, kbeg + (long)t * BK, p.N, wave, lane);
+    glds_tile<128, BT>(st + HALF, B, p.ldb, n0 + 128, kbeg + (long)t * BK, p.N, wave, lane);
+  };
+  const int bcol = (wc & 1) * 64;  // first column of this wave inside its B half
+  auto readA = [&](bf16x8 (&af)[4][2], const char* la, int mh) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][kk] = read_frag<128, AT>(la, 64 * mh + 16 * i, kk, lane);
+  };
+  auto readB = [&](bf16x8 (&bq)[2][2], const char* lb, int nh) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bq[j][kk] = read_frag<128, BT>(lb, bcol + 32 * nh + 16 * j, kk, lane);
+  };
+  auto quad = [&](const bf16x8 (&af)[4][2], const bf16x8 (&bq)[2][2], int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * mh + i][2 * nh + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bq[j][kk], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define OWLK_PP_BAR() asm volatile("s_barrier" ::: "memory")
+#define OWLK_PP_SYNC() asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory")
+
+  issueA(0);
+  issueB(0);
+  if (nk > 1) {
+    issueB(1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  OWLK_PP_BAR();
+  if (wr == 1) OWLK_PP_BAR();  // group 1 runs one barrier behind group 0
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const char* la = smem + (t & 1) * STAGE + wr * HALF;
+    const char* lb = smem + (t & 1) * STAGE + (2 + (wc >> 1)) * HALF;
+    // phase 0
+    readB(b0, lb, 0);
+    readA(af, la, 0);
+    if (t + 1 < nk) issueA(t + 1);
+    OWLK_PP_SYNC();
+    quad(af, b0, 0, 0);
+    OWLK_PP_BAR();
+    // phase 1
+    readB(b1, lb, 1);
+    OWLK_PP_SYNC();
+    quad(af, b1, 0, 1);
+    OWLK_PP_BAR();
+    // phase 2
+    readA(af, la, 1);
+    OWLK_PP_SYNC();
+    quad(af, b1, 1, 1);
+    OWLK_PP_BAR();
+    // phase 3
+    if (t + 2 < nk) {
+      issueB(t + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    OWLK_PP_SYNC();
+    quad(af, b0, 1, 0);
+    OWLK_PP_BAR();
+  }
+  if (wr == 0) OWLK_PP_BAR();  // pairs with group 1's final barrier: every MFMA / LDS read done
+#undef OWLK_PP_BAR
+#undef OWLK_PP_SYNC
+
+  // ---- epilogue per wave through a private 16 x 64 fp32 LDS strip (reuses the staging ring)
+  const long wrow0 = m0 + 128 * wr, wcol0 = n0 + 64 * wc;
+  float* strip = (float*)smem + wave * (16 * 68);
+  const bool atomic = OF32 && EPI == EPI_STORE && gridDim.y > 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * 68 + 16 * j + (lane & 15)] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const long rbase = wrow0 + 16 * i;
+    if (atomic) {
+      float* C = (float*)p.C + z * p.sC;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const long gm = rbase + rr;
+        if (gm < p.M) atomicAdd(C + gm * p.ldc + wcol0 + lane, p.alpha * strip[rr * 68 + lane]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = lane + 64 * q;
+        const int rr = c >> 3, col = (c & 7) * 8;
+        const long gm = rbase + rr, gn = wcol0 + col;
+        float v[8];
+        const f32x4 lo = *(const f32x4*)(strip + rr * 68 + col);
+        const f32x4 hi = *(const f32x4*)(strip + rr * 68 + col + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lo[e];
+          v[e + 4] = hi[e];
+        }
+        if (gm < p.M) epi_chunk<EPI, OF32>(p, z, gm, gn, v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 template <int BM, int BN, bool AT, bool BT, int EPI, bool OF32>
 int launch(GemmP& p, long batch, hipStream_t s) {
   p.tiles_m = (int)((p.M + BM - 1) / BM);
@@ -501,7 +670,11 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
   p.tiles_n = (int)((p.N + 255) / 256);
   const int splits = (int)((p.K + p.kchunk - 1) / p.kchunk);
   dim3 grid(p.tiles_m * p.tiles_n, (unsigned)splits, (unsigned)batch);
-  hipLaunchKernelGGL((gemm256_kernel<256, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  static const int pp = getenv("OWLK_GEMM_PP") ? atoi(getenv("OWLK_GEMM_PP")) : 1;
+  if (pp)
+    hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<256, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   return owlk::check_launch("gemm256");
 }
 

@@ -53,6 +53,39 @@ def test_gemm_layouts(M, N, K_, at, bt):
     assert rel(outb, ref) < 5e-3
 
 
+@pytest.mark.parametrize("K_", [64, 128, 192, 1536])
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
+def test_gemm256_pingpong(K_, at, bt):
+    """>= 256 tiles of 256^2 route to the ping-pong LDS-DMA kernel: K-tile counts 1, 2, 3 (ring
+    prologue / drain edge cases) and 24, every operand layout, rows clamped on a ragged M."""
+    M, N = 4096 + (0 if at else 40), 4096
+    A = rnd(K_, M, seed=11) if at else rnd(M, K_, seed=11)
+    B = rnd(K_, N, seed=12) if bt else rnd(N, K_, seed=12)
+    ref = (A.float().T if at else A.float()) @ (B.float() if bt else B.float().T)
+    out = K().gemm(A, B, a_trans=at, b_trans=bt, out_f32=True)
+    assert rel(out, ref) < 1e-5
+
+
+def test_gemm256_epilogues():
+    """fused epilogues on the 256^2 ping-pong path (dit_v4-like widths)."""
+    k = K()
+    M, N, Kd, tpf = 8192, 2048, 512, 64
+    A, W = rnd(M, Kd, seed=13), rnd(N, Kd, scale=0.1, seed=14)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    acc = A.float() @ W.float().T
+    y = (acc + bias.bfloat16().float()).bfloat16().float()
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    s = k.gemm(A, W, bias=bias, epi=k.EPI_SILU, aux=aux)
+    assert rel(aux, y) < 5e-3 and rel(s, torch.nn.functional.silu(y)) < 5e-3
+    g, res = rnd(M // tpf, N, seed=15), rnd(M, N, seed=16)
+    o = k.gemm(A, W, bias=bias, epi=k.EPI_GATE_RESID, aux=aux, gate=g, tpf=tpf, resid=res)
+    assert rel(o, res.float() + g.float().repeat_interleave(tpf, 0) * y) < 5e-3 and rel(aux, y) < 5e-3
+    x = res.float()
+    sg = torch.sigmoid(x)
+    d = k.gemm(A, W, epi=k.EPI_DSILU, aux=res)
+    assert rel(d, acc * sg * (1 + x * (1 - sg))) < 5e-3
+
+
 def test_gemm_epilogues():
     k = K()
     M, N, Kd, tpf = 512, 256, 192, 64
