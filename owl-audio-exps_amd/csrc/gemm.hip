@@ -185,6 +185,73 @@ DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
   }
 }
 
+// epi_chunk with the bias (already bf16-rounded, bb) and the aux / resid (x) and gate (g) inputs
+// supplied by the caller (loaded ahead of time)
+template <int EPI, bool OF32>
+DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], const float (&bb)[8], const bf16x8& x,
+                   const bf16x8& g) {
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
+    if (OF32) {
+      float* C = (float*)p.C + z * p.sC + gm * p.ldc + gn;
+      if (p.beta != 0.f) {
+        const f32x4 o0 = *(const f32x4*)C, o1 = *(const f32x4*)(C + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += p.beta * o0[e];
+          v[e + 4] += p.beta * o1[e];
+        }
+      }
+      *(f32x4*)C = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      bf16* C = (bf16*)p.C + z * p.sC + gm * p.ldc + gn;
+      if (p.beta != 0.f) {
+        float o[8];
+        unpack8(*(const bf16x8*)C, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += p.beta * o[e];
+      }
+      *(bf16x8*)C = pack8(v);
+    }
+  } else if (EPI == EPI_SILU) {
+    float y[8], s[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      y[e] = rb(v[e] + bb[e]);
+      s[e] = silu_f(y[e]);
+    }
+    *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(s);
+  } else if (EPI == EPI_GATE_RESID) {
+    float y[8], gg[8], r[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = rb(v[e] + bb[e]);
+    unpack8(g, gg);
+    unpack8(x, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = r[e] + rb(gg[e] * y[e]);
+    if (p.aux) *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  } else if (EPI == EPI_DSILU) {
+    float xx[8], o[8];
+    unpack8(x, xx);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sg = 1.f / (1.f + __expf(-xx[e]));
+      o[e] = rb(v[e]) * sg * (1.f + xx[e] * (1.f - sg));
+    }
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  } else if (EPI == EPI_AXPBY) {
+    float xx[8], o[8];
+    unpack8(x, xx);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * xx[e]));
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  }
+}
+
 template <int BM, int BN, bool AT, bool BT, int EPI, bool OF32>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;  // wave tile
@@ -590,12 +657,46 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
 #undef OWLK_PP_BAR
 #undef OWLK_PP_SYNC
 
-  // ---- epilogue per wave through a private 16 x 64 fp32 LDS strip (reuses the staging ring)
+  // ---- epilogue per wave through a private 16 x 64 fp32 LDS strip (reuses the staging ring).
+  // Each lane owns one 8-column chunk (fixed for the whole tile): its bias is loaded once, and the
+  // aux / resid / gate inputs of strip i + 1 are loaded while strip i is formatted and stored, so
+  // no strip waits a full global-load latency (per-strip loads cost ~10 us per tile-round).
   const long wrow0 = m0 + 128 * wr, wcol0 = n0 + 64 * wc;
   float* strip = (float*)smem + wave * (16 * 68);
   const bool atomic = OF32 && EPI == EPI_STORE && gridDim.y > 1;
+  const int ccol = (lane & 7) * 8;
+  const long gn = wcol0 + ccol;
+  float bb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bb[e] = 0.f;
+  if (!atomic && p.bias) {
+    const f32x4 lo = *(const f32x4*)(p.bias + gn), hi = *(const f32x4*)(p.bias + gn + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bb[e] = rb(lo[e]);
+      bb[e + 4] = rb(hi[e]);
+    }
+  }
+  constexpr bool HAS_X = EPI == EPI_GATE_RESID || EPI == EPI_DSILU || EPI == EPI_AXPBY;
+  constexpr bool HAS_G = EPI == EPI_GATE_RESID;
+  bf16x8 xin[2][2], gin[2][2];  // [strip parity][q]
+  auto load_in = [&](int i, bf16x8 (&x)[2], bf16x8 (&g)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      long gm = wrow0 + 16 * i + 8 * q + (lane >> 3);
+      gm = gm < p.M ? gm : p.M - 1;
+      if (HAS_X) {
+        const bf16* src = EPI == EPI_GATE_RESID ? p.resid + z * p.sRes + gm * p.ldres
+                                                 : p.aux + z * p.sAux + gm * p.ldaux;
+        x[q] = *(const bf16x8*)(src + gn);
+      }
+      if (HAS_G) g[q] = *(const bf16x8*)(p.gate + z * p.sGate + (long)((unsigned)gm / (unsigned)p.tpf) * p.ldgate + gn);
+    }
+  };
+  if (!atomic) load_in(0, xin[0], gin[0]);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
+    if (!atomic && i + 1 < 8) load_in(i + 1, xin[(i + 1) & 1], gin[(i + 1) & 1]);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -612,18 +713,17 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
     } else {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int c = lane + 64 * q;
-        const int rr = c >> 3, col = (c & 7) * 8;
-        const long gm = rbase + rr, gn = wcol0 + col;
+        const int rr = 8 * q + (lane >> 3);
+        const long gm = rbase + rr;
         float v[8];
-        const f32x4 lo = *(const f32x4*)(strip + rr * 68 + col);
-        const f32x4 hi = *(const f32x4*)(strip + rr * 68 + col + 4);
+        const f32x4 lo = *(const f32x4*)(strip + rr * 68 + ccol);
+        const f32x4 hi = *(const f32x4*)(strip + rr * 68 + ccol + 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           v[e] = lo[e];
           v[e + 4] = hi[e];
         }
-        if (gm < p.M) epi_chunk<EPI, OF32>(p, z, gm, gn, v);
+        if (gm < p.M) epi_apply<EPI, OF32>(p, z, gm, gn, v, bb, xin[i & 1][q], gin[i & 1][q]);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
