@@ -31,6 +31,17 @@ DEV s16x4 ds_read_tr16(const void* lds_byte_ptr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_ptr)(lds_byte_ptr));
 }
 
+// Same instruction through inline asm: invisible to the waitcnt pass.  The builtin above carries
+// no LDS alias scope, so after any LDS-DMA (global_load_lds) hipcc puts an s_waitcnt vmcnt(0)
+// before the first such read -- draining a DMA ring that is meant to stay in flight.  The CALLER
+// must retire these reads itself (s_waitcnt lgkmcnt(0) + sched_barrier before the consumer).
+DEV s16x4 ds_read_tr16_async(const void* lds_byte_ptr) {
+  s16x4 r;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_byte_ptr;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
 DEV bf16x8 join_tr(s16x4 lo, s16x4 hi) {
   union { s16x4 s[2]; bf16x8 v; } u;
   u.s[0] = lo;

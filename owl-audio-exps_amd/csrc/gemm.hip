@@ -117,6 +117,20 @@ DEV bf16x8 read_frag(const char* lds, int row0, int kk, int lane) {
   }
 }
 
+// read_frag with the transposed reads issued through inline asm (ds_read_tr16_async): the caller
+// retires them with its own s_waitcnt lgkmcnt(0) before the MFMAs (ping-pong kernel)
+template <int ROWS, bool TRANS>
+DEV bf16x8 read_frag_async(const char* lds, int row0, int kk, int lane) {
+  if (!TRANS) return read_frag<ROWS, false>(lds, row0, kk, lane);
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int blk = row0 >> 4;
+  const int k0 = 32 * kk + 8 * g + q;
+  const int k1 = k0 + 4;
+  s16x4 lo = ds_read_tr16_async(lds + k0 * (ROWS * 2) + ((blk ^ swz_t<ROWS>(k0)) << 5) + pp * 8);
+  s16x4 hi = ds_read_tr16_async(lds + k1 * (ROWS * 2) + ((blk ^ swz_t<ROWS>(k1)) << 5) + pp * 8);
+  return join_tr(lo, hi);
+}
+
 // epilogue for 8 consecutive outputs C[gm, gn .. gn + 8) of batch item z (v = raw accumulators)
 template <int EPI, bool OF32>
 DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
@@ -587,13 +601,13 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i][kk] = read_frag<128, AT>(la, 64 * mh + 16 * i, kk, lane);
+      for (int i = 0; i < 4; ++i) af[i][kk] = read_frag_async<128, AT>(la, 64 * mh + 16 * i, kk, lane);
   };
   auto readB = [&](bf16x8 (&bq)[2][2], const char* lb, int nh) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bq[j][kk] = read_frag<128, BT>(lb, bcol + 32 * nh + 16 * j, kk, lane);
+      for (int j = 0; j < 2; ++j) bq[j][kk] = read_frag_async<128, BT>(lb, bcol + 32 * nh + 16 * j, kk, lane);
   };
   auto quad = [&](const bf16x8 (&af)[4][2], const bf16x8 (&bq)[2][2], int mh, int nh) {
     __builtin_amdgcn_s_setprio(1);
@@ -608,7 +622,11 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
     __builtin_amdgcn_s_setprio(0);
   };
 #define OWLK_PP_BAR() asm volatile("s_barrier" ::: "memory")
-#define OWLK_PP_SYNC() asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory")
+#define OWLK_PP_SYNC()                                                  \
+  do {                                                                  \
+    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");   \
+    __builtin_amdgcn_sched_barrier(0);                                  \
+  } while (0)
 
   issueA(0);
   issueB(0);
