@@ -114,6 +114,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   const bool wave_live = kw0 < p.Lkv;
   const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
   const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
+  TileRange full = full_range_q(m, wfk0, wfk1, qbeg, p.Lq, TL);
+  if (!wave_live || kw0 + 32 > p.Lkv) full = TileRange{1, 0};
+  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
+  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
 
   f32x16 dk[C::NDB], dv[C::NDB];
 #pragma unroll
@@ -163,10 +167,13 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
     const float* l2 = (const float*)(lq + 2 * C::NSUB * SUB);
     const float* dlt = l2 + TL;
 
-    const long qlast = (q0 + TL - 1 < p.Lq ? q0 + TL - 1 : p.Lq - 1);
-    int kind = TILE_EMPTY;
-    if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
-    if (kind == TILE_FULL && (q0 + TL > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
+    int kind = TILE_FULL;
+    if (t < full.lo || t >= full.hi) {
+      const long qlast = (q0 + TL - 1 < p.Lq ? q0 + TL - 1 : p.Lq - 1);
+      kind = TILE_EMPTY;
+      if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
+      if (kind == TILE_FULL && (q0 + TL > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
+    }
     kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {
@@ -281,6 +288,10 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
   const bool wave_live = r0 < p.Lq;
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
+  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, TL);
+  if (!wave_live) full = TileRange{1, 0};
+  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
+  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
 
   f32x16 dq[C::NDB];
 #pragma unroll
@@ -317,10 +328,13 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
     if (t + C::NBUF - 1 < ntiles) issue(smem + ((t + C::NBUF - 1) % C::NBUF) * BUF, c0 + (long)(C::NBUF - 1) * TL);
     const char* lk = smem + (t % C::NBUF) * BUF;
     const char* lv = lk + C::NSUB * SUB;
-    const long clast = (c0 + TL - 1 < p.Lkv ? c0 + TL - 1 : p.Lkv - 1);
-    int kind = TILE_EMPTY;
-    if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
-    if (kind == TILE_FULL && c0 + TL > p.Lkv) kind = TILE_PARTIAL;
+    int kind = TILE_FULL;
+    if (t < full.lo || t >= full.hi) {
+      const long clast = (c0 + TL - 1 < p.Lkv ? c0 + TL - 1 : p.Lkv - 1);
+      kind = TILE_EMPTY;
+      if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
+      if (kind == TILE_FULL && c0 + TL > p.Lkv) kind = TILE_PARTIAL;
+    }
     kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {

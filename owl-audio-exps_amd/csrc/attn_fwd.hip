@@ -118,6 +118,10 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const bool wave_live = r0 < p.Lq;
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
+  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, KT);
+  if (!wave_live) full = TileRange{1, 0};
+  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
+  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
 
   f32x16 o[C::NDB];
 #pragma unroll
@@ -159,10 +163,13 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
     const char* lk = smem + (t % C::NBUF) * C::TILEB;
     const char* lv = lk + C::NSUB * SUB;
 
-    const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
-    int kind = TILE_EMPTY;
-    if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
-    if (kind == TILE_FULL && c0 + KT > p.Lkv) kind = TILE_PARTIAL;
+    int kind = TILE_FULL;
+    if (t < full.lo || t >= full.hi) {
+      const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
+      kind = TILE_EMPTY;
+      if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
+      if (kind == TILE_FULL && c0 + KT > p.Lkv) kind = TILE_PARTIAL;
+    }
     kind = __builtin_amdgcn_readfirstlane(kind);  // wave-uniform: scalar branch, no exec masking
 
     if (kind != TILE_EMPTY) {
