@@ -64,8 +64,11 @@ template <int D>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) {
   using C = Cfg<D>;
   constexpr int BUF = 2 * C::NSUB * SUB + 2 * TL * 4;  // Q | dO | lse2 | delta
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF];
-  __shared__ int red_hi;
+  // ONE __shared__ object (the reduction slot sits past the ring): with a second one hipcc tags
+  // the LDS-DMA with an alias scope and drains the ring (vmcnt(0)) before the first ds_read of
+  // every tile (cdna_hip_programming.md §5 item 4(a))
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF + 16];
+  int& red_hi = *(int*)(smem + C::NBUF * BUF);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const BlockIds bid = xcd_block_ids();
@@ -238,8 +241,8 @@ template <int D>
 __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
   using C = Cfg<D>;
   constexpr int BUF = 2 * C::NSUB * SUB;  // K | V
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF];
-  __shared__ int red_lo;
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF + 16];  // + reduction slot (one object)
+  int& red_lo = *(int*)(smem + C::NBUF * BUF);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const BlockIds bid = xcd_block_ids();

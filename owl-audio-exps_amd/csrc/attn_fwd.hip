@@ -58,8 +58,11 @@ DEV void vmcnt() {
 template <int D, bool BOUNDED>
 __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   using C = Cfg<D>;
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::TILEB];
-  __shared__ int red_lo;
+  // ONE __shared__ object (the reduction slot sits past the ring): with a second one hipcc tags
+  // the LDS-DMA with an alias scope and drains the ring (vmcnt(0)) before the first ds_read of
+  // every tile (cdna_hip_programming.md §5 item 4(a))
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::TILEB + 16];
+  int& red_lo = *(int*)(smem + C::NBUF * C::TILEB);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const BlockIds bid = xcd_block_ids();
