@@ -14,6 +14,8 @@
 // natural lse * log2 e): the backward's P = exp2(c s - lse2) then needs no conversion.
 #include "attn_common.hpp"
 
+#include <cstdlib>
+
 
 namespace {
 
@@ -263,8 +265,232 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   }
 }
 
+// D = 64 with 64 query rows per wave (two 32-row blocks qb): every K fragment (ds_read_b128)
+// and every V^T fragment (ds_read_b64_tr_b16) read from LDS feeds two MFMAs, and the per-tile
+// fixed costs (DMA issue, ring bookkeeping, classification, barrier) are paid once per 32
+// MFMAs instead of 16.  Workgroup = 4 waves = 256 query rows; ~200 VGPRs -> 2 waves per SIMD.
+constexpr int QT2 = 256;
+template <bool BOUNDED>
+__global__ __launch_bounds__(256, 2) void attn_fwd2_k(FwdP p) {
+  using C = Cfg<64>;
+  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::TILEB + 16];
+  int& red_lo = *(int*)(smem + C::NBUF * C::TILEB);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, ql = lane & 31;
+  const BlockIds bid = xcd_block_ids();
+  const long b = bid.z;
+  const int head = bid.y;
+  const int ntq = (int)((p.Lq + QT2 - 1) / QT2);
+  const long q0 = (long)(ntq - 1 - bid.x) * QT2;  // heaviest (latest) query tiles first
+  const long r0 = q0 + 64 * w;                     // this wave's first row
+  const MaskP& m = p.m;
+
+  const bf16* Q = p.q + b * p.sqb + head * 64;
+  const bf16* K = p.k + b * p.skb + head * 64;
+  const bf16* V = p.v + b * p.svb + head * 64;
+
+  const long qlast = (q0 + QT2 < p.Lq ? q0 + QT2 : p.Lq) - 1;
+  const int fq_lo = frame_of(m, q0 + m.q_offset), fq_hi = frame_of(m, qlast + m.q_offset);
+  int lo_f;
+  if (m.kv_lo) {
+    if (threadIdx.x == 0) red_lo = 1 << 30;
+    __syncthreads();
+    int mn = 1 << 30;
+    for (int f = fq_lo + threadIdx.x; f <= fq_hi; f += 256) mn = min(mn, m.kv_lo[b * m.fstride + f]);
+    atomicMin(&red_lo, mn);
+    __syncthreads();
+    lo_f = red_lo;
+  } else {
+    lo_f = m.window > 0 ? max(0, fq_lo - m.window + 1) : 0;
+  }
+  int hi_f = m.causal ? fq_hi : (m.window > 0 ? min(m.n_frames - 1, fq_hi + m.window - 1) : m.n_frames - 1);
+  long kv_begin = (long)lo_f * m.tpf;
+  long kv_end = ((long)hi_f + 1) * m.tpf;
+  if (kv_end > p.Lkv) kv_end = p.Lkv;
+  kv_begin = (kv_begin / KT) * KT;
+  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + KT - 1) / KT) : 0;
+
+  // query fragments of both row blocks (B operand of S^T = K Q^T)
+  long my_q[2];
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    my_q[qb] = r0 + 32 * qb + ql;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[qb][s] = my_q[qb] < p.Lq ? *(const bf16x8*)(Q + my_q[qb] * p.ldq + 16 * s + 8 * h) : bf16x8{};
+    if constexpr (BOUNDED) {  // q' = bf16(q c): see attn_fwd_k
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float f[8];
+        unpack8(qf[qb][s], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= p.scale_log2;
+        qf[qb][s] = pack8(f);
+      }
+    }
+  }
+  const long wlast = (r0 + 63 < p.Lq ? r0 + 63 : p.Lq - 1);
+  const bool wave_live = r0 < p.Lq;
+  const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
+  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, KT);
+  if (!wave_live) full = TileRange{1, 0};
+  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
+  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
+
+  f32x16 o[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) o[qb][0] = o[qb][1] = f32x16{};
+  float mrow[2] = {BOUNDED ? 0.f : -INFINITY, BOUNDED ? 0.f : -INFINITY}, lrow[2] = {0.f, 0.f};
+
+  const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_TR>(p.ldv, w, lane);
+  auto issue = [&](char* buf, long c0) {
+    if (c0 + KT <= p.Lkv) {
+      tile_glds_fast(buf, K + c0 * p.ldk, goff_k, w);
+      tile_glds_fast(buf + SUB, V + c0 * p.ldv, goff_v, w);
+    } else {
+      tile_glds<SW_ROW>(buf, K, p.ldk, c0, p.Lkv, w, lane);
+      tile_glds<SW_TR>(buf + SUB, V, p.ldv, c0, p.Lkv, w, lane);
+    }
+  };
+  auto wait_oldest = [&](int younger) {
+    if (younger > 0)
+      vmcnt<C::OPS>();
+    else
+      vmcnt<0>();
+  };
+#pragma unroll
+  for (int i = 0; i < C::NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * C::TILEB, kv_begin + (long)i * KT);
+  wait_oldest(min(C::NBUF - 2, ntiles - 1));
+  OWLK_BARRIER();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const long c0 = kv_begin + (long)t * KT;
+    if (t + C::NBUF - 1 < ntiles)
+      issue(smem + ((t + C::NBUF - 1) % C::NBUF) * C::TILEB, c0 + (long)(C::NBUF - 1) * KT);
+    const char* lk = smem + (t % C::NBUF) * C::TILEB;
+    const char* lv = lk + SUB;
+
+    int kind = TILE_FULL;
+    if (t < full.lo || t >= full.hi) {
+      const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
+      kind = TILE_EMPTY;
+      if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
+      if (kind == TILE_FULL && c0 + KT > p.Lkv) kind = TILE_PARTIAL;
+    }
+    kind = __builtin_amdgcn_readfirstlane(kind);
+
+    if (kind != TILE_EMPTY) {
+      const bool masked = kind == TILE_PARTIAL;
+      // S^T[key][q] for 2 key blocks x 2 query blocks; each K fragment feeds both query blocks
+      f32x16 st[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        st[kb][0] = st[kb][1] = f32x16{};
+        const int krow = 32 * kb + ql;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = *(const bf16x8*)(lk + krow * 128 + (((2 * s + h) ^ swz_row(krow)) << 4));
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            st[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][s], st[kb][qb], 0, 0, 0);
+        }
+      }
+      if (masked) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          const unsigned long long bh = tile_bits(m, b, my_q[qb], my_q[qb] < p.Lq, c0, p.Lkv, true) >> (4 * h);
+          apply_bits<0>(st[0][qb], bh, -INFINITY);
+          apply_bits<32>(st[1][qb], bh, -INFINITY);
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float mc = 0.f;
+        if constexpr (!BOUNDED) {
+          float tmax = -INFINITY;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[kb][qb][r]);
+          tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+          const float mnew = fmaxf(mrow[qb], tmax);
+          mc = mnew == -INFINITY ? 0.f : mnew * p.scale_log2;
+          if (__any(mnew > mrow[qb])) {
+            const float alpha = __builtin_amdgcn_exp2f(mrow[qb] * p.scale_log2 - mc);
+            lrow[qb] *= alpha;
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) o[qb][db][r] *= alpha;
+          }
+          mrow[qb] = mnew;
+        }
+        // row sums in four independent partial sums (no 32-long dependent add chain)
+        float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = BOUNDED ? __builtin_amdgcn_exp2f(st[kb][qb][r])
+                                     : __builtin_amdgcn_exp2f(fmaf(st[kb][qb][r], p.scale_log2, -mc));
+            st[kb][qb][r] = pv;
+            ps[r & 3] += pv;
+          }
+        lrow[qb] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      }
+      // O^T[d][q] += V^T[d][key] P^T[key][q]: each V^T fragment feeds both query blocks
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf0 = acc_frag(st[kb][0], s), pf1 = acc_frag(st[kb][1], s);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const bf16x8 vt = frag_tr<SW_TR>(lv, 32 * kb, s, db, lane);
+            o[0][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vt, pf0, o[0][db], 0, 0, 0);
+            o[1][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vt, pf1, o[1][db], 0, 0, 0);
+          }
+        }
+    }
+    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));
+    OWLK_BARRIER();
+  }
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const float ltot = lrow[qb] + __shfl_xor(lrow[qb], 32, 64);
+    if (my_q[qb] < p.Lq) {
+      const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+      bf16* O = p.o + b * p.sob + my_q[qb] * p.ldo + head * 64;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          bf16x4 v4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[qb][db][4 * gq + e] * inv);
+          *(bf16x4*)(O + 32 * db + 8 * gq + 4 * h) = v4;
+        }
+      if (h == 0)
+        p.lse[(b * p.H + head) * p.Lq + my_q[qb]] =
+            ltot > 0.f ? mrow[qb] * p.scale_log2 + __log2f(ltot) : -INFINITY;
+    }
+  }
+}
+
 template <int D>
 void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
+  static const int two = getenv("OWLK_FWD2") ? atoi(getenv("OWLK_FWD2")) : 1;
+  if (D == 64 && two) {
+    const dim3 g2((unsigned)((p.Lq + QT2 - 1) / QT2), grid.y, grid.z);
+    if (p.bound > 0.f)
+      hipLaunchKernelGGL((attn_fwd2_k<true>), g2, dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_fwd2_k<false>), g2, dim3(256), 0, s, p);
+    return;
+  }
   if (p.bound > 0.f)
     hipLaunchKernelGGL((attn_fwd_k<D, true>), grid, dim3(256), 0, s, p);
   else
