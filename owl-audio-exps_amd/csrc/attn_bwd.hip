@@ -114,6 +114,24 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
     kf[s] = my_k < p.Lkv ? *(const bf16x8*)(K + my_k * p.ldk + 16 * s + 8 * h) : bf16x8{};
     vf[s] = my_k < p.Lkv ? *(const bf16x8*)(V + my_k * p.ldv + 16 * s + 8 * h) : bf16x8{};
   }
+  // Row constants ride in the accumulators: k' = bf16(-c k), v' = -v, and the S / dP chains start
+  // from lse2 / delta, so  acc_s = lse2 - c s  (P = exp2(-acc_s), the negation a free input
+  // modifier of v_exp) and  acc_p = delta - dP = -(dP - delta).  That removes the per-score FMA
+  // and subtraction; dK = scale dS^T Q picks up the sign (stored with -scale).  k' rounds c k to
+  // bf16 once (the forward rounded c q instead: the same 2^-9 relative level).
+#pragma unroll
+  for (int s = 0; s < C::NS; ++s) {
+    float f[8], g[8];
+    unpack8(kf[s], f);
+    unpack8(vf[s], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] *= -p.scale_log2;
+      g[j] = -g[j];
+    }
+    kf[s] = pack8(f);
+    vf[s] = pack8(g);
+  }
   const bool wave_live = kw0 < p.Lkv;
   const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
   const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
@@ -185,7 +203,18 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
       if (masked) bh = tile_bits(m, b, my_k, my_k < p.Lkv, q0, p.Lq, false) >> (4 * h);
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
-        f32x16 st = f32x16{}, dp = f32x16{};
+        f32x16 st, dp;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {  // rows acc_row(4 g4 + e, h) = rowb + e
+          const int rowb = 32 * qb + 8 * g4 + 4 * h;
+          const f32x4 L = *(const f32x4*)(l2 + rowb);
+          const f32x4 Dl = *(const f32x4*)(dlt + rowb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            st[4 * g4 + e] = L[e];
+            dp[4 * g4 + e] = Dl[e];
+          }
+        }
 #pragma unroll
         for (int s = 0; s < C::NS; ++s) {
           st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq + (s >> 2) * SUB, 32 * qb, s & 3, lane),
@@ -194,17 +223,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
                                                        vf[s], dp, 0, 0, 0);
         }
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int rowb = 32 * qb + 8 * g4 + 4 * h;  // rows acc_row(4 g4 + e, h) = rowb + e
-          const f32x4 L = *(const f32x4*)(l2 + rowb);
-          const f32x4 Dl = *(const f32x4*)(dlt + rowb);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g4 + e;
-            st[r] = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L[e]));
-            dp[r] -= Dl[e];
-          }
-        }
+        for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(-st[r]);
         if (masked) {
           if (qb == 0)
             apply_bits<0>(st, bh, 0.f);
@@ -231,7 +250,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   }
 
   if (my_k < p.Lkv) {
-    store_rowT<C::NDB>(p.dk + b * p.sdkb + my_k * p.lddk + head * D, dk, p.scale, h);
+    store_rowT<C::NDB>(p.dk + b * p.sdkb + my_k * p.lddk + head * D, dk, -p.scale, h);  // dS was accumulated negated
     store_rowT<C::NDB>(p.dv + b * p.sdvb + my_k * p.lddv + head * D, dv, 1.f, h);
   }
 }
