@@ -257,7 +257,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
 
 // ======================================================================== dQ
 template <int D>
-__global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
+#ifndef OWLK_DQ_INIT
+#define OWLK_DQ_INIT 1
+#endif
+__global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void attn_bwd_dq_k(BwdP p) {
+  constexpr bool INIT = OWLK_DQ_INIT && D == 64;
   using C = Cfg<D>;
   constexpr int BUF = 2 * C::NSUB * SUB;  // K | V
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF + 16];  // + reduction slot (one object)
@@ -307,6 +311,25 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
   }
   const float L2 = qok ? p.lse[(b * p.H + head) * p.Lq + my_q] : 0.f;  // base-2 lse (attn_fwd)
   const float Dl = qok ? p.delta[(b * p.H + head) * p.Lq + my_q] : 0.f;
+  // OWLK_DQ_INIT: q' = bf16(c q) and constant accumulator-init registers -lse2 / -delta (the
+  // first MFMA of each chain reads them as C), so S' arrives as the exp2 argument and dP - delta
+  // needs no subtraction: 2 VALU per score instead of 4, for 32 more VGPRs (2 waves / SIMD)
+  f32x16 sinit, pinit;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    sinit[r] = -L2;
+    pinit[r] = -Dl;
+  }
+  if (INIT) {
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) {
+      float f[8];
+      unpack8(qf[s], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= p.scale_log2;
+      qf[s] = pack8(f);
+    }
+  }
   const bool wave_live = r0 < p.Lq;
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
@@ -365,7 +388,7 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
       if (masked) bh = tile_bits(m, b, my_q, qok, c0, p.Lkv, true) >> (4 * h);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        f32x16 st = f32x16{}, dp = f32x16{};
+        f32x16 st = INIT ? sinit : f32x16{}, dp = INIT ? pinit : f32x16{};
 #pragma unroll
         for (int s = 0; s < C::NS; ++s) {
           st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lk + (s >> 2) * SUB, 32 * kb, s & 3, lane),
@@ -374,7 +397,8 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
                                                        df[s], dp, 0, 0, 0);
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L2));
+        for (int r = 0; r < 16; ++r)
+          st[r] = INIT ? __builtin_amdgcn_exp2f(st[r]) : __builtin_amdgcn_exp2f(fmaf(st[r], p.scale_log2, -L2));
         if (masked) {
           if (kb == 0)
             apply_bits<0>(st, bh, 0.f);
@@ -382,7 +406,7 @@ __global__ __launch_bounds__(256, D == 64 ? 3 : 2) void attn_bwd_dq_k(BwdP p) {
             apply_bits<32>(st, bh, 0.f);
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dp[r] = st[r] * (dp[r] - Dl);
+        for (int r = 0; r < 16; ++r) dp[r] = INIT ? st[r] * dp[r] : st[r] * (dp[r] - Dl);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const bf16x8 sf = acc_frag(dp, s);
