@@ -60,15 +60,30 @@ DEV void store_rowT(bf16* dst, const f32x16 (&acc)[NDB], float mul, int h) {
 }
 
 // ======================================================================== dK, dV
-template <int D>
+// Query tiles of QT x 64 rows per ring slot.  QT = 2 (D 64, unwindowed masks: two-slot ring,
+// 66 KiB per workgroup, two workgroups per CU) pays the per-tile fixed costs (DMA issue, ring
+// bookkeeping, the workgroup barrier) once per 64 MFMAs: global layers -2.5 %.  Windowed (local)
+// layers keep QT = 1 and the three-slot ring: their short sweeps are dominated by mask-edge
+// tiles, which QT = 2 makes twice as large (+60 % measured there).
+template <int D, int QT_>
+struct DkdvCfg {
+  static constexpr int QT = QT_;
+  static constexpr int NBUF = QT == 2 ? 2 : Cfg<D>::NBUF;
+  static constexpr int TLQ = TL * QT;  // query rows per tile
+};
+
+template <int D, int QT_>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) {
   using C = Cfg<D>;
-  constexpr int BUF = 2 * C::NSUB * SUB + 2 * TL * 4;  // Q | dO | lse2 | delta
+  using G = DkdvCfg<D, QT_>;
+  constexpr int QT = G::QT, TLQ = G::TLQ, NBUF = G::NBUF;
+  constexpr int BUF = 2 * QT * C::NSUB * SUB + 2 * TLQ * 4;  // Q [QT] | dO [QT] | lse2 | delta
+  constexpr int LSEW = TLQ / 64;                              // waves moving one 256-B lse2 row each
   // ONE __shared__ object (the reduction slot sits past the ring): with a second one hipcc tags
   // the LDS-DMA with an alias scope and drains the ring (vmcnt(0)) before the first ds_read of
   // every tile (cdna_hip_programming.md §5 item 4(a))
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF + 16];
-  int& red_hi = *(int*)(smem + C::NBUF * BUF);
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + 16];
+  int& red_hi = *(int*)(smem + NBUF * BUF);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const BlockIds bid = xcd_block_ids();
@@ -104,7 +119,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   long qbeg = ((long)fq_start * m.tpf / TL) * TL;
   long qend = ((long)fq_end + 1) * m.tpf;
   if (qend > p.Lq) qend = p.Lq;
-  const int ntiles = qend > qbeg ? (int)((qend - qbeg + TL - 1) / TL) : 0;
+  const int ntiles = qend > qbeg ? (int)((qend - qbeg + TLQ - 1) / TLQ) : 0;
 
   // ---- this wave's K and V as B operands (key on the lane): X[key][16 s + 8 h ..]
   const long my_k = kw0 + ql;
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   const bool wave_live = kw0 < p.Lkv;
   const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
   const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
-  TileRange full = full_range_q(m, wfk0, wfk1, qbeg, p.Lq, TL);
+  TileRange full = full_range_q(m, wfk0, wfk1, qbeg, p.Lq, TLQ);
   if (!wave_live || kw0 + 32 > p.Lkv) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
@@ -144,108 +159,121 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
 #pragma unroll
   for (int db = 0; db < C::NDB; ++db) dk[db] = dv[db] = f32x16{};
 
-  // Q / dO tiles + the lse2 / delta rows arrive by LDS-DMA into the ring: per tile every wave
-  // issues 2 x 1 KiB per sub-tile of Q and of dO (its 16 rows), waves 0 / 1 one 256-B row each
-  // (lse2 / delta); offsets are per-lane constants, bases wave-uniform.
+  // Q / dO sub-tiles + the lse2 / delta rows arrive by LDS-DMA into the ring: per 64-row sub-tile
+  // every wave issues 2 x 1 KiB per column sub-tile of Q and of dO (its 16 rows); waves
+  // 0 .. 2 LSEW - 1 one 256-B row of lse2 / delta each; offsets are per-lane constants.
   const GldsOff go_q = glds_offsets<SW_DUAL>(p.ldq, w, lane), go_d = glds_offsets<SW_DUAL>(p.ldo, w, lane);
   auto issue = [&](char* buf, long q0) {
-    const bool inner = q0 + TL <= p.Lq;
 #pragma unroll
-    for (int sb = 0; sb < C::NSUB; ++sb) {
-      if (inner) {
-        tile_glds_fast(buf + sb * SUB, Q + q0 * p.ldq + 64 * sb, go_q, w);
-        tile_glds_fast(buf + (C::NSUB + sb) * SUB, dO + q0 * p.ldo + 64 * sb, go_d, w);
-      } else {
-        tile_glds<SW_DUAL>(buf + sb * SUB, Q + 64 * sb, p.ldq, q0, p.Lq, w, lane);
-        tile_glds<SW_DUAL>(buf + (C::NSUB + sb) * SUB, dO + 64 * sb, p.ldo, q0, p.Lq, w, lane);
+    for (int sq = 0; sq < QT; ++sq) {
+      const long r = q0 + 64 * sq;
+      char* bq = buf + sq * C::NSUB * SUB;
+      char* bd = buf + (QT + sq) * C::NSUB * SUB;
+#pragma unroll
+      for (int sb = 0; sb < C::NSUB; ++sb) {
+        if (r + TL <= p.Lq) {
+          tile_glds_fast(bq + sb * SUB, Q + r * p.ldq + 64 * sb, go_q, w);
+          tile_glds_fast(bd + sb * SUB, dO + r * p.ldo + 64 * sb, go_d, w);
+        } else {
+          tile_glds<SW_DUAL>(bq + sb * SUB, Q + 64 * sb, p.ldq, r, p.Lq, w, lane);
+          tile_glds<SW_DUAL>(bd + sb * SUB, dO + 64 * sb, p.ldo, r, p.Lq, w, lane);
+        }
       }
     }
-    if (w < 2) {
-      const long n = p.Lq - q0;
-      const int i = inner ? lane : (lane < n ? lane : (int)n - 1);  // ragged tail: clamp (masked later)
-      glds_f32(buf + 2 * C::NSUB * SUB + w * TL * 4, (w == 0 ? LSE : DLT) + q0 + i);
+    if (w < 2 * LSEW) {
+      const int part = w >> 1;  // 64-row part of the lse2 / delta vectors
+      const long r = q0 + 64 * part;
+      const long n = p.Lq - r;
+      const int i = r + 64 <= p.Lq ? lane : (lane < n ? lane : (n > 0 ? (int)n - 1 : 0));  // ragged: clamp
+      const long src = r + i < p.Lq ? r + i : p.Lq - 1;
+      glds_f32(buf + 2 * QT * C::NSUB * SUB + ((w & 1) * TLQ + 64 * part) * 4, ((w & 1) ? DLT : LSE) + src);
     }
   };
+  constexpr int OPS = 4 * QT * C::NSUB;  // 16-B LDS-DMA wave-instructions per tile per wave
   auto wait_oldest = [&](int younger) {  // this wave's share of the oldest issued tile landed
     if (younger <= 0)
       vmcnt<0>();
-    else if (w < 2)
-      vmcnt<C::OPS + 1>();
+    else if (w < 2 * LSEW)
+      vmcnt<OPS + 1>();
     else
-      vmcnt<C::OPS>();
+      vmcnt<OPS>();
   };
 #pragma unroll
-  for (int i = 0; i < C::NBUF - 1; ++i)
-    if (i < ntiles) issue(smem + i * BUF, qbeg + (long)i * TL);
-  wait_oldest(min(C::NBUF - 2, ntiles - 1));
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * BUF, qbeg + (long)i * TLQ);
+  wait_oldest(min(NBUF - 2, ntiles - 1));
   OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
-    const long q0 = qbeg + (long)t * TL;
-    if (t + C::NBUF - 1 < ntiles) issue(smem + ((t + C::NBUF - 1) % C::NBUF) * BUF, q0 + (long)(C::NBUF - 1) * TL);
-    const char* lq = smem + (t % C::NBUF) * BUF;
-    const char* ld = lq + C::NSUB * SUB;
-    const float* l2 = (const float*)(lq + 2 * C::NSUB * SUB);
-    const float* dlt = l2 + TL;
+    const long q0 = qbeg + (long)t * TLQ;
+    if (t + NBUF - 1 < ntiles) issue(smem + ((t + NBUF - 1) % NBUF) * BUF, q0 + (long)(NBUF - 1) * TLQ);
+    const char* tb = smem + (t % NBUF) * BUF;
+    const float* l2 = (const float*)(tb + 2 * QT * C::NSUB * SUB);
+    const float* dlt = l2 + TLQ;
 
     int kind = TILE_FULL;
     if (t < full.lo || t >= full.hi) {
-      const long qlast = (q0 + TL - 1 < p.Lq ? q0 + TL - 1 : p.Lq - 1);
+      const long qlast = (q0 + TLQ - 1 < p.Lq ? q0 + TLQ - 1 : p.Lq - 1);
       kind = TILE_EMPTY;
       if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
-      if (kind == TILE_FULL && (q0 + TL > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
+      if (kind == TILE_FULL && (q0 + TLQ > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
     }
     kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
-      unsigned long long bh = 0ull;
-      if (masked) bh = tile_bits(m, b, my_k, my_k < p.Lkv, q0, p.Lq, false) >> (4 * h);
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        f32x16 st, dp;
+      for (int sq = 0; sq < QT; ++sq) {
+        const char* lq = tb + sq * C::NSUB * SUB;
+        const char* ld = tb + (QT + sq) * C::NSUB * SUB;
+        unsigned long long bh = 0ull;
+        if (masked) bh = tile_bits(m, b, my_k, my_k < p.Lkv, q0 + 64 * sq, p.Lq, false) >> (4 * h);
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {  // rows acc_row(4 g4 + e, h) = rowb + e
-          const int rowb = 32 * qb + 8 * g4 + 4 * h;
-          const f32x4 L = *(const f32x4*)(l2 + rowb);
-          const f32x4 Dl = *(const f32x4*)(dlt + rowb);
+        for (int qb = 0; qb < 2; ++qb) {
+          f32x16 st, dp;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            st[4 * g4 + e] = L[e];
-            dp[4 * g4 + e] = Dl[e];
+          for (int g4 = 0; g4 < 4; ++g4) {  // rows acc_row(4 g4 + e, h) = rowb + e
+            const int rowb = 64 * sq + 32 * qb + 8 * g4 + 4 * h;
+            const f32x4 L = *(const f32x4*)(l2 + rowb);
+            const f32x4 Dl = *(const f32x4*)(dlt + rowb);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              st[4 * g4 + e] = L[e];
+              dp[4 * g4 + e] = Dl[e];
+            }
           }
-        }
 #pragma unroll
-        for (int s = 0; s < C::NS; ++s) {
-          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq + (s >> 2) * SUB, 32 * qb, s & 3, lane),
-                                                       kf[s], st, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(ld + (s >> 2) * SUB, 32 * qb, s & 3, lane),
-                                                       vf[s], dp, 0, 0, 0);
-        }
+          for (int s = 0; s < C::NS; ++s) {
+            st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq + (s >> 2) * SUB, 32 * qb, s & 3, lane),
+                                                         kf[s], st, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(ld + (s >> 2) * SUB, 32 * qb, s & 3, lane),
+                                                         vf[s], dp, 0, 0, 0);
+          }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(-st[r]);
-        if (masked) {
-          if (qb == 0)
-            apply_bits<0>(st, bh, 0.f);
-          else
-            apply_bits<32>(st, bh, 0.f);
-        }
+          for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(-st[r]);
+          if (masked) {
+            if (qb == 0)
+              apply_bits<0>(st, bh, 0.f);
+            else
+              apply_bits<32>(st, bh, 0.f);
+          }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dp[r] *= st[r];
+          for (int r = 0; r < 16; ++r) dp[r] *= st[r];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 pf = acc_frag(st, s), sf = acc_frag(dp, s);
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 pf = acc_frag(st, s), sf = acc_frag(dp, s);
 #pragma unroll
-          for (int db = 0; db < C::NDB; ++db) {
-            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                frag_tr<SW_DUAL>(ld + (db >> 1) * SUB, 32 * qb, s, db & 1, lane), pf, dv[db], 0, 0, 0);
-            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                frag_tr<SW_DUAL>(lq + (db >> 1) * SUB, 32 * qb, s, db & 1, lane), sf, dk[db], 0, 0, 0);
+            for (int db = 0; db < C::NDB; ++db) {
+              dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                  frag_tr<SW_DUAL>(ld + (db >> 1) * SUB, 32 * qb, s, db & 1, lane), pf, dv[db], 0, 0, 0);
+              dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                  frag_tr<SW_DUAL>(lq + (db >> 1) * SUB, 32 * qb, s, db & 1, lane), sf, dk[db], 0, 0, 0);
+            }
           }
         }
       }
     }
-    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));
+    wait_oldest(min(NBUF - 2, ntiles - 2 - t));
     OWLK_BARRIER();
   }
 
@@ -426,8 +454,15 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
 template <int D>
 int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipStream_t s) {
   if (phases & 1) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_k<D>, dim3((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B),
-                       dim3(256), 0, s, p);
+    const dim3 grid((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B);
+    if constexpr (D == 64) {
+      if (p.m.window <= 0)
+        hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2>), grid, dim3(256), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1>), grid, dim3(256), 0, s, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1>), grid, dim3(256), 0, s, p);
+    }
     if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
   }
   if (phases & 2) {

@@ -187,6 +187,7 @@ ATTN_CASES = [
     (1, 2, 5, 65, 2, False),
     (2, 1, 9, 4, 3, True),
     (1, 2, 24, 64, 16, True),
+    (1, 2, 7, 65, None, False),  # unwindowed, ragged inside the second 64-row half of a 128-row dK/dV tile
 ]
 
 
