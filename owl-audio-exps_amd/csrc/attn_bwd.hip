@@ -284,16 +284,19 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
 }
 
 // ======================================================================== dQ
-template <int D>
+// Key tiles of QT x 64 rows per ring slot: QT = 2 (D 64, unwindowed masks; two-slot ring) pays the
+// per-tile fixed costs once per 48 MFMAs, as in the dK/dV kernel.
 #ifndef OWLK_DQ_INIT
 #define OWLK_DQ_INIT 1
 #endif
+template <int D, int QT>
 __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void attn_bwd_dq_k(BwdP p) {
   constexpr bool INIT = OWLK_DQ_INIT && D == 64;
   using C = Cfg<D>;
-  constexpr int BUF = 2 * C::NSUB * SUB;  // K | V
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * BUF + 16];  // + reduction slot (one object)
-  int& red_lo = *(int*)(smem + C::NBUF * BUF);
+  constexpr int NBUF = QT == 2 ? 2 : C::NBUF, TLK = TL * QT;
+  constexpr int BUF = 2 * QT * C::NSUB * SUB;  // K [QT] | V [QT]
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + 16];  // + reduction slot (one object)
+  int& red_lo = *(int*)(smem + NBUF * BUF);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = lane >> 5, ql = lane & 31;
   const BlockIds bid = xcd_block_ids();
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
   long kv_begin = ((long)lo_f * m.tpf / TL) * TL;
   long kv_end = ((long)hi_f + 1) * m.tpf;
   if (kv_end > p.Lkv) kv_end = p.Lkv;
-  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + TL - 1) / TL) : 0;
+  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + TLK - 1) / TLK) : 0;
 
   const long my_q = r0 + ql;
   const bool qok = my_q < p.Lq;
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
   const bool wave_live = r0 < p.Lq;
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, TL);
+  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, TLK);
   if (!wave_live) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
@@ -374,46 +377,56 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
   const GldsOff go_k = glds_offsets<SW_DUAL>(p.ldk, w, lane), go_v = glds_offsets<SW_ROW>(p.ldv, w, lane);
   auto issue = [&](char* buf, long c0) {
 #pragma unroll
-    for (int sb = 0; sb < C::NSUB; ++sb) {
-      if (c0 + TL <= p.Lkv) {
-        tile_glds_fast(buf + sb * SUB, K + c0 * p.ldk + 64 * sb, go_k, w);
-        tile_glds_fast(buf + (C::NSUB + sb) * SUB, V + c0 * p.ldv + 64 * sb, go_v, w);
-      } else {
-        tile_glds<SW_DUAL>(buf + sb * SUB, K + 64 * sb, p.ldk, c0, p.Lkv, w, lane);
-        tile_glds<SW_ROW>(buf + (C::NSUB + sb) * SUB, V + 64 * sb, p.ldv, c0, p.Lkv, w, lane);
+    for (int sk = 0; sk < QT; ++sk) {
+      const long c = c0 + 64 * sk;
+      char* bk = buf + sk * C::NSUB * SUB;
+      char* bv = buf + (QT + sk) * C::NSUB * SUB;
+#pragma unroll
+      for (int sb = 0; sb < C::NSUB; ++sb) {
+        if (c + TL <= p.Lkv) {
+          tile_glds_fast(bk + sb * SUB, K + c * p.ldk + 64 * sb, go_k, w);
+          tile_glds_fast(bv + sb * SUB, V + c * p.ldv + 64 * sb, go_v, w);
+        } else {
+          tile_glds<SW_DUAL>(bk + sb * SUB, K + 64 * sb, p.ldk, c, p.Lkv, w, lane);
+          tile_glds<SW_ROW>(bv + sb * SUB, V + 64 * sb, p.ldv, c, p.Lkv, w, lane);
+        }
       }
     }
   };
+  constexpr int OPS = 4 * QT * C::NSUB;  // 16-B LDS-DMA wave-instructions per tile per wave
   auto wait_oldest = [&](int younger) {
     if (younger > 0)
-      vmcnt<C::OPS>();
+      vmcnt<OPS>();
     else
       vmcnt<0>();
   };
 #pragma unroll
-  for (int i = 0; i < C::NBUF - 1; ++i)
-    if (i < ntiles) issue(smem + i * BUF, kv_begin + (long)i * TL);
-  wait_oldest(min(C::NBUF - 2, ntiles - 1));
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * BUF, kv_begin + (long)i * TLK);
+  wait_oldest(min(NBUF - 2, ntiles - 1));
   OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
-    const long c0 = kv_begin + (long)t * TL;
-    if (t + C::NBUF - 1 < ntiles) issue(smem + ((t + C::NBUF - 1) % C::NBUF) * BUF, c0 + (long)(C::NBUF - 1) * TL);
-    const char* lk = smem + (t % C::NBUF) * BUF;
-    const char* lv = lk + C::NSUB * SUB;
+    const long c0 = kv_begin + (long)t * TLK;
+    if (t + NBUF - 1 < ntiles) issue(smem + ((t + NBUF - 1) % NBUF) * BUF, c0 + (long)(NBUF - 1) * TLK);
+    const char* tb = smem + (t % NBUF) * BUF;
     int kind = TILE_FULL;
     if (t < full.lo || t >= full.hi) {
-      const long clast = (c0 + TL - 1 < p.Lkv ? c0 + TL - 1 : p.Lkv - 1);
+      const long clast = (c0 + TLK - 1 < p.Lkv ? c0 + TLK - 1 : p.Lkv - 1);
       kind = TILE_EMPTY;
       if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
-      if (kind == TILE_FULL && c0 + TL > p.Lkv) kind = TILE_PARTIAL;
+      if (kind == TILE_FULL && c0 + TLK > p.Lkv) kind = TILE_PARTIAL;
     }
     kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
+#pragma unroll
+      for (int sk = 0; sk < QT; ++sk) {
+      const char* lk = tb + sk * C::NSUB * SUB;
+      const char* lv = tb + (QT + sk) * C::NSUB * SUB;
       unsigned long long bh = 0ull;
-      if (masked) bh = tile_bits(m, b, my_q, qok, c0, p.Lkv, true) >> (4 * h);
+      if (masked) bh = tile_bits(m, b, my_q, qok, c0 + 64 * sk, p.Lkv, true) >> (4 * h);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         f32x16 st = INIT ? sinit : f32x16{}, dp = INIT ? pinit : f32x16{};
@@ -444,8 +457,9 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
                 frag_tr<SW_DUAL>(lk + (db >> 1) * SUB, 32 * kb, s, db & 1, lane), sf, dq[db], 0, 0, 0);
         }
       }
+      }  // sk
     }
-    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));
+    wait_oldest(min(NBUF - 2, ntiles - 2 - t));
     OWLK_BARRIER();
   }
   if (qok) store_rowT<C::NDB>(p.dq + b * p.sdqb + my_q * p.lddq + head * D, dq, p.scale, h);
@@ -466,8 +480,15 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
     if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
   }
   if (phases & 2) {
-    hipLaunchKernelGGL(attn_bwd_dq_k<D>, dim3((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B), dim3(256),
-                       0, s, p);
+    const dim3 grid((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B);
+    if constexpr (D == 64) {
+      if (p.m.window <= 0)
+        hipLaunchKernelGGL((attn_bwd_dq_k<D, 2>), grid, dim3(256), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
+    }
     if (int e = owlk::check_launch("attn_bwd_dq")) return e;
   }
   return 0;
