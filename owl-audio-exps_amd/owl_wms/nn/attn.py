@@ -35,7 +35,12 @@ def get_block_mask(n_tokens, tokens_per_frame, window_len=None, doc_id=None, q_o
     arrays = None
     if doc_id is not None:
         n_frames = (n_tokens + tokens_per_frame - 1) // tokens_per_frame
-        arrays = K.frame_arrays(doc_id.to(device), n_frames, window_len, is_causal)
+        doc = doc_id.to(device)[:, :n_frames]
+        # one document per sample (the unpacked case): the doc_id predicate of mask_mod is always
+        # true, so the kernels take the document-free path (analytic FULL-tile ranges, no
+        # per-frame array reads in the tile loop)
+        if not bool((doc == doc[:, :1]).all()):
+            arrays = K.frame_arrays(doc, n_frames, window_len, is_causal)
     return K.FrameMask(tokens_per_frame, window_len, is_causal, q_offset, arrays)
 
 
