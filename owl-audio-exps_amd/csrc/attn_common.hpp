@@ -113,11 +113,40 @@ DEV bool allowed(const MaskP& m, long b, int fq, int fk) {
 // 64-bit allowed-mask of one lane against a 64-row tile of the other side: bit i set iff
 // (self, other0 + i) is allowed.  self_is_query selects which side `self` indexes.  Only built
 // for PARTIAL tiles, so the FULL-tile hot path carries no mask arithmetic at all.
+DEV unsigned long long range_bits(long lo, long hi) {  // bits [lo, hi) of 0..63 (clamped)
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > 64 ? 64 : hi;
+  if (hi <= lo) return 0ull;
+  const unsigned long long upto = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  return upto & ~((1ull << lo) - 1ull);
+}
+
 DEV unsigned long long tile_bits(const MaskP& m, long b, long self, bool self_ok, long other0, long other_len,
                                  bool self_is_query) {
   unsigned long long bits = 0ull;
   if (!self_ok) return 0ull;
   const int fs = frame_of(m, self + (self_is_query ? m.q_offset : 0));
+  if (!m.doc) {
+    // without documents the allowed other-side rows are one contiguous index range: causal and
+    // window bounds are monotone in the other side's frame (a 64-step per-element loop cost more
+    // than the tile's MFMAs)
+    const long tpf = m.tpf, W = m.window;
+    long lo = 0, hi = other_len;
+    if (self_is_query) {  // other = keys, frame(k) in [fs - W + 1, fs] (causal) / (fs - W, fs + W)
+      if (m.causal) hi = min(hi, ((long)fs + 1) * tpf);
+      if (W > 0) {
+        lo = max(lo, ((long)fs - W + 1) * tpf);
+        if (!m.causal) hi = min(hi, ((long)fs + W) * tpf);
+      }
+    } else {  // other = queries (frame of o + q_offset), self = key frame fs
+      if (m.causal) lo = max(lo, (long)fs * tpf - m.q_offset);
+      if (W > 0) {
+        hi = min(hi, ((long)fs + W) * tpf - m.q_offset);
+        if (!m.causal) lo = max(lo, ((long)fs - W + 1) * tpf - m.q_offset);
+      }
+    }
+    return range_bits(lo - other0, hi - other0);
+  }
   for (int i = 0; i < 64; ++i) {
     const long o = other0 + i;
     if (o >= other_len) break;
