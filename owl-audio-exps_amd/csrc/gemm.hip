@@ -199,6 +199,9 @@ DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
   }
 }
 
+// streaming output chunk: non-temporal 16-B store (epilogue outputs are not re-read by this kernel)
+DEV void st_nt(bf16x8* dst, bf16x8 v) { __builtin_nontemporal_store(v, dst); }
+
 // epi_chunk with the bias (already bf16-rounded, bb) and the aux / resid (x) and gate (g) inputs
 // supplied by the caller (loaded ahead of time)
 template <int EPI, bool OF32>
@@ -227,7 +230,7 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += p.beta * o[e];
       }
-      *(bf16x8*)C = pack8(v);
+      st_nt((bf16x8*)C, pack8(v));
     }
   } else if (EPI == EPI_SILU) {
     float y[8], s[8];
@@ -236,8 +239,8 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
       y[e] = rb(v[e] + bb[e]);
       s[e] = silu_f(y[e]);
     }
-    *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
-    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(s);
+    st_nt((bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), pack8(y));
+    st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(s));
   } else if (EPI == EPI_GATE_RESID) {
     float y[8], gg[8], r[8], o[8];
 #pragma unroll
@@ -246,8 +249,8 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
     unpack8(x, r);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = r[e] + rb(gg[e] * y[e]);
-    if (p.aux) *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(y);
-    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    if (p.aux) st_nt((bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), pack8(y));
+    st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
   } else if (EPI == EPI_DSILU) {
     float xx[8], o[8];
     unpack8(x, xx);
@@ -256,13 +259,13 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
       const float sg = 1.f / (1.f + __expf(-xx[e]));
       o[e] = rb(v[e]) * sg * (1.f + xx[e] * (1.f - sg));
     }
-    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
   } else if (EPI == EPI_AXPBY) {
     float xx[8], o[8];
     unpack8(x, xx);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * xx[e]));
-    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
   }
 }
 
