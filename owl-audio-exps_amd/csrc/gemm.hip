@@ -700,7 +700,9 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
   }
   constexpr bool HAS_X = EPI == EPI_GATE_RESID || EPI == EPI_DSILU || EPI == EPI_AXPBY;
   constexpr bool HAS_G = EPI == EPI_GATE_RESID;
-  bf16x8 xin[2][2], gin[2][2];  // [strip parity][q]
+  // prefetch depth (strips): every input of the tile up front where registers allow
+  constexpr int PD = (EPI == EPI_DSILU || EPI == EPI_AXPBY) ? 8 : (EPI == EPI_GATE_RESID ? 4 : 1);
+  bf16x8 xin[8][2], gin[8][2];  // [strip][q]
   auto load_in = [&](int i, bf16x8 (&x)[2], bf16x8 (&g)[2]) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -714,10 +716,13 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
       if (HAS_G) g[q] = *(const bf16x8*)(p.gate + z * p.sGate + (long)((unsigned)gm / (unsigned)p.tpf) * p.ldgate + gn);
     }
   };
-  if (!atomic) load_in(0, xin[0], gin[0]);
+  if (!atomic) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) load_in(i, xin[i], gin[i]);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    if (!atomic && i + 1 < 8) load_in(i + 1, xin[(i + 1) & 1], gin[(i + 1) & 1]);
+    if (!atomic && i + PD < 8) load_in(i + PD, xin[i + PD], gin[i + PD]);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -744,7 +749,7 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
           v[e] = lo[e];
           v[e + 4] = hi[e];
         }
-        if (gm < p.M) epi_apply<EPI, OF32>(p, z, gm, gn, v, bb, xin[i & 1][q], gin[i & 1][q]);
+        if (gm < p.M) epi_apply<EPI, OF32>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q]);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
