@@ -14,7 +14,9 @@
 // through LDS so every global access is a 16-B row chunk.
 #include "common.hpp"
 
+#include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 namespace {
 
@@ -40,7 +42,8 @@ struct GemmP {
   const bf16* gate; long ldgate, sGate, tpf;
   const bf16* resid; long ldres, sRes;
   int tiles_m, tiles_n;
-  long kchunk;  // split-K: K range per blockIdx.y (multiple of BK); fp32 atomics combine the splits
+  long kchunk;  // split-K: K range per blockIdx.y (multiple of BK)
+  float* ws;    // split-K partials [split][M][N] (256^2 kernel); null: fp32 atomics combine the splits
 };
 
 // 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
@@ -729,7 +732,17 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
       for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * 68 + 16 * j + (lane & 15)] = acc[i][j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const long rbase = wrow0 + 16 * i;
-    if (atomic) {
+    if (atomic && p.ws) {
+      // this split's partial, unscaled: 16 B per lane, 4 rows x 256 B per wave-instruction
+      float* W = p.ws + (long)blockIdx.y * p.M * p.N;
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        const int rr = 4 * rq + (lane >> 4);
+        const long gm = rbase + rr;
+        if (gm < p.M)
+          *(f32x4*)(W + gm * p.N + wcol0 + 4 * (lane & 15)) = *(const f32x4*)(strip + rr * 68 + 4 * (lane & 15));
+      }
+    } else if (atomic) {
       float* C = (float*)p.C + z * p.sC;
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
@@ -825,6 +838,57 @@ int dispatch256(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStre
   owlk::set_error("gemm: unknown epilogue %d", epi);
   return 1;
 }
+// C[m, n] = alpha sum_s W[s][m, n] + beta C[m, n] (beta 0: C is not read); N % 4 == 0
+__global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__ W, int splits, long M, long N,
+                                                       float* C, long ldc, float alpha, float beta) {
+  const long nq = N / 4, total = M * nq, MN = M * N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long m = i / nq, n = (i - m * nq) * 4;
+    const float* w = W + m * N + n;
+    f32x4 a = __builtin_nontemporal_load((const f32x4*)w);
+    for (int sp = 1; sp < splits; ++sp) {
+      const f32x4 b = __builtin_nontemporal_load((const f32x4*)(w + sp * MN));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += b[e];
+    }
+    f32x4* c = (f32x4*)(C + m * ldc + n);
+    f32x4 o;
+    if (beta != 0.f) {
+      const f32x4 old = *c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = alpha * a[e] + beta * old[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = alpha * a[e];
+    }
+    *c = o;
+  }
+}
+
+// grow-only split-K workspace per device; growth drains the device before freeing the old one
+float* splitk_workspace(size_t bytes) {
+  static std::mutex mu;
+  static void* buf[64] = {};
+  static size_t cap[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (cap[dev] < bytes) {
+    if (buf[dev]) {
+      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+      (void)hipFree(buf[dev]);
+      buf[dev] = nullptr;
+      cap[dev] = 0;
+    }
+    if (hipMalloc(&buf[dev], bytes) != hipSuccess) {
+      buf[dev] = nullptr;
+      return nullptr;
+    }
+    cap[dev] = bytes;
+  }
+  return (float*)buf[dev];
+}
+
 // split-K factor for long reductions onto few 256^2 tiles (weight gradients, K = tokens): at one
 // workgroup per CU (128 KiB LDS) the grid runs in ceil(tiles * s / 256) rounds, so pick s to fill
 // the last round (e.g. 144 tiles: s = 4 -> 2.25 rounds, 75 % of the third idle; s = 7 -> 3.94);
@@ -883,21 +947,43 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   const bool fits256 = use256 && K % 64 == 0 && N % 256 == 0 && (!a_trans || M % 256 == 0) &&
                        (!b_trans || N % 256 == 0) && !(c_f32 && beta != 0.f && beta != 1.f);
   if (fits256) {
-    if (c_f32 && epi == EPI_STORE && beta == 1.f && K >= 8192 && tiles256 < 1024) {
+    // split-K onto an fp32 output: partials to a workspace + one reduce pass (any beta), or with
+    // OWLK_GEMM_ATOMIC=1 fp32 atomics into a caller-zeroed output (beta 1)
+    static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
+    if (c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && tiles256 < 1024) {
       const long splits = pick_splits(tiles256, K);
       if (splits > 1) {
         p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
-        return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
+        const long nsp = (K + p.kchunk - 1) / p.kchunk;
+        if (atomic_splitk) {
+          if (beta == 0.f)
+            OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
+                         "gemm: clearing the split-K output failed");
+          return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
+        }
+        p.ws = splitk_workspace((size_t)nsp * M * N * sizeof(float));
+        OWLK_REQUIRE(p.ws, "gemm: split-K workspace of %ld x %ld x %ld fp32 not allocated", nsp, M, N);
+        if (int e = dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s)) return e;
+        const long work = M * (N / 4);
+        const unsigned grid = (unsigned)std::min<long>((work + 255) / 256, 2048);
+        hipLaunchKernelGGL(splitk_reduce_k, dim3(grid), dim3(256), 0, s, p.ws, (int)nsp, M, N, (float*)C, ldc,
+                           alpha, beta);
+        return owlk::check_launch("splitk_reduce");
       }
     }
     if (tiles256 >= 256) return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
   }
   // long reductions onto small outputs (weight gradients, K = tokens): 128x128 tiles, K split so
-  // the grid covers ~4 workgroups per CU; the fp32 output must be zeroed by the caller (beta = 1)
-  if (c_f32 && epi == EPI_STORE && beta == 1.f && K >= 8192 && tiles128 < 1024) {
+  // the grid covers ~4 workgroups per CU; fp32 atomics onto a caller-zeroed (beta 1) or cleared (beta 0) C
+  if (c_f32 && epi == EPI_STORE && (beta == 1.f || (beta == 0.f && batch == 1)) && K >= 8192 && tiles128 < 1024) {
     long splits = (1024 + tiles128 - 1) / tiles128;
     if (splits > K / 4096) splits = K / 4096;
     if (splits > 1) {
+      if (beta == 0.f) {  // the atomics add onto C: clear it first
+        OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
+                     "gemm: clearing the split-K output failed");
+        p.beta = 1.f;
+      }
       p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
       return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
     }

@@ -58,8 +58,8 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
 
 def gemm_wgrad(dy, x):
     """fp32 weight gradient dW[n, k] = sum_m dy[m, n] x[m, k] (split-K over the token dimension)."""
-    out = torch.zeros(dy.shape[1], x.shape[1], device=dy.device, dtype=F32)
-    return gemm(dy, x, a_trans=True, b_trans=True, out=out, out_f32=True, beta=1.0)
+    out = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=F32)
+    return gemm(dy, x, a_trans=True, b_trans=True, out=out, out_f32=True, beta=0.0)
 
 
 def bgemm(A, B, out, *, a_trans=False, b_trans=False, epi=EPI_STORE, alpha=1.0, beta=0.0, aux=None):

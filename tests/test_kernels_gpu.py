@@ -308,13 +308,30 @@ def test_newton_schulz_matches_oracle(shape):
     assert (sv - sr).abs().max() < 0.05
 
 
-@pytest.mark.parametrize("M,N,K_", [(128, 1536, 16384), (1536, 1536, 20480), (4608, 256, 12288)])
+@pytest.mark.parametrize("M,N,K_", [(128, 1536, 16384), (1536, 1536, 20480), (4608, 256, 12288),
+                                     (1536, 2048, 24576)])
 def test_gemm_splitk_weight_grad(M, N, K_):
     k = K()
     dy, x = rnd(K_, M, seed=70), rnd(K_, N, seed=71)
     ref = dy.float().T @ x.float()
     out = k.gemm_wgrad(dy, x)
     assert rel(out, ref) < 1e-5
+
+
+def test_gemm_splitk_workspace_alpha_beta():
+    """256^2 split-K (48 tiles x 12 splits): partials + reduce give alpha AB + beta C; beta 0 never
+    reads C (NaN-filled here)."""
+    k = K()
+    M, N, K_ = 1536, 2048, 24576
+    dy, x = rnd(K_, M, seed=72), rnd(K_, N, seed=73)
+    ref = dy.float().T @ x.float()
+    out = torch.full((M, N), float("nan"), device=DEV)
+    k.gemm(dy, x, a_trans=True, b_trans=True, out=out, out_f32=True, beta=0.0)
+    assert rel(out, ref) < 1e-5
+    c0 = torch.randn(M, N, device=DEV)
+    out = c0.clone()
+    k.gemm(dy, x, a_trans=True, b_trans=True, out=out, out_f32=True, alpha=0.5, beta=1.0)
+    assert rel(out, 0.5 * ref + c0) < 1e-5
 
 
 def test_frame_mux_roundtrip():

@@ -36,6 +36,7 @@ def main():
         ("fc2 dX", r(T, d), r(d, 4 * d), False, True),
         ("qkv dX", r(T, 3 * d), r(3 * d, d), False, True),
         ("fc1 dW", r(T, 4 * d), r(T, d), True, True),
+        ("fc2 dW", r(T, d), r(T, 4 * d), True, True),
         ("qkv dW", r(T, 3 * d), r(T, d), True, True),
         ("out dW", r(T, d), r(T, d), True, True),
     ]
