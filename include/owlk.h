@@ -29,8 +29,12 @@ int owlk_device_ok(void);
  *       3 DSILU      C = bf16(bf16(acc) * silu'(aux))
  *       4 AXPBY      C = bf16(bf16(alpha * bf16(acc)) + bf16(beta * aux))
  *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes.
- *   fp32 STORE with beta == 1 and K >= 8192 onto a small output (weight gradients) splits K over
- *   workgroups and combines with fp32 atomics: C must hold the accumulation base (e.g. zeros). */
+ *   fp32 STORE with beta 0 or 1 and K >= 8192 onto a small output (weight gradients) splits K
+ *   over workgroups; the per-split partials go to a library-owned device workspace (grown on
+ *   first use, never shrunk) and one fixed-order reduce forms C, so the result is deterministic.
+ *   colsum (optional, batch 1, bf16 C): colsum[n] += sum_m C[m, n] over the stored bf16 values
+ *   (bias gradient of the next layer, fused into the DSILU epilogue of the 256^2 kernel; a
+ *   separate column-sum pass otherwise).  Caller zeroes it. */
 int owlk_gemm(long M, long N, long K, long batch,
               const void* A, long lda, long sA, int a_trans,
               const void* B, long ldb, long sB, int b_trans,
@@ -39,7 +43,7 @@ int owlk_gemm(long M, long N, long K, long batch,
               void* aux, long ldaux, long sAux,
               const void* gate, long ldgate, long sGate, long tpf,
               const void* resid, long ldres, long sRes,
-              void* stream);
+              float* colsum, void* stream);
 
 /* ---- AdaLN modulate (modulation.py:7-26 AdaLN.forward after its fc; :46-55 cond_adaln):
  *   y[t] = bf16(bf16(bf16(rms_norm(x[t])) * bf16(1 + scale[t/tpf])) + shift[t/tpf]); rstd[t] fp32 */

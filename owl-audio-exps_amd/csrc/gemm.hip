@@ -44,6 +44,8 @@ struct GemmP {
   int tiles_m, tiles_n;
   long kchunk;  // split-K: K range per blockIdx.y (multiple of BK)
   float* ws;    // split-K partials [split][M][N] (256^2 kernel); null: fp32 atomics combine the splits
+  float* colsum_req;  // caller wants colsum[n] += sum_m C[m, n] (stored bf16 values)
+  float* colsum;      // ... and the launched kernel fuses it (set by the dispatch, else a separate pass)
 };
 
 // 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
@@ -209,7 +211,7 @@ DEV void st_nt(bf16x8* dst, bf16x8 v) { __builtin_nontemporal_store(v, dst); }
 // supplied by the caller (loaded ahead of time)
 template <int EPI, bool OF32>
 DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], const float (&bb)[8], const bf16x8& x,
-                   const bf16x8& g) {
+                   const bf16x8& g, float (&cs)[8]) {
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
@@ -263,6 +265,10 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
       o[e] = rb(v[e]) * sg * (1.f + xx[e] * (1.f - sg));
     }
     st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
+    if (p.colsum) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += rb(o[e]);
+    }
   } else if (EPI == EPI_AXPBY) {
     float xx[8], o[8];
     unpack8(x, xx);
@@ -723,6 +729,9 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < PD; ++i) load_in(i, xin[i], gin[i]);
   }
+  float cs[8];  // fused column sums of the stored outputs (EPI_DSILU with p.colsum)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (!atomic && i + PD < 8) load_in(i + PD, xin[i + PD], gin[i + PD]);
@@ -762,10 +771,24 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
           v[e] = lo[e];
           v[e + 4] = hi[e];
         }
-        if (gm < p.M) epi_apply<EPI, OF32>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q]);
+        if (gm < p.M) epi_apply<EPI, OF32>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (EPI == EPI_DSILU && p.colsum) {
+    // lanes l, l + 8, ..., l + 56 hold the same 8 columns: butterfly over lane bits 3..5, then
+    // one fp32 atomic per column per wave (2 waves x tiles_m adders per column)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      cs[e] += __shfl_xor(cs[e], 8, 64);
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(p.colsum + gn + e, cs[e]);
+    }
   }
 }
 
@@ -810,6 +833,8 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
   const int splits = (int)((p.K + p.kchunk - 1) / p.kchunk);
   dim3 grid(p.tiles_m * p.tiles_n, (unsigned)splits, (unsigned)batch);
   static const int pp = getenv("OWLK_GEMM_PP") ? atoi(getenv("OWLK_GEMM_PP")) : 1;
+  static const int fuse_cs = getenv("OWLK_GEMM_COLSUM") ? atoi(getenv("OWLK_GEMM_COLSUM")) : 1;
+  if (pp && EPI == EPI_DSILU && batch == 1 && fuse_cs) p.colsum = p.colsum_req;
   if (pp)
     hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   else
@@ -912,7 +937,7 @@ long pick_splits(long tiles, long K) {
 }
 }  // namespace
 
-extern "C" int owlk_gemm(long M, long N, long K, long batch,
+static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
                          const void* A, long lda, long sA, int a_trans,
                          const void* B, long ldb, long sB, int b_trans,
                          void* C, long ldc, long sC, int c_f32,
@@ -930,7 +955,6 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   OWLK_REQUIRE(!c_f32 || epi == EPI_STORE, "gemm: fp32 output only with EPI_STORE");
   OWLK_REQUIRE(epi != EPI_GATE_RESID || (gate && resid && tpf > 0), "gemm: gate epilogue needs gate/resid/tpf");
   OWLK_REQUIRE(!(epi == EPI_SILU || epi == EPI_DSILU || epi == EPI_AXPBY) || aux, "gemm: epilogue needs aux");
-  GemmP p{};
   p.M = M; p.N = N; p.K = K;
   p.A = (const bf16*)A; p.lda = lda; p.sA = sA;
   p.B = (const bf16*)B; p.ldb = ldb; p.sB = sB;
@@ -991,4 +1015,25 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   // small outputs (per-frame modulation, Newton-Schulz) use 64x64 tiles to fill the chip
   if (tiles128 < 512) return dispatch_e<64, 64>(p, a_trans, b_trans, epi, c_f32, batch, s);
   return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
+}
+
+extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream);
+
+extern "C" int owlk_gemm(long M, long N, long K, long batch,
+                         const void* A, long lda, long sA, int a_trans,
+                         const void* B, long ldb, long sB, int b_trans,
+                         void* C, long ldc, long sC, int c_f32,
+                         int epi, float alpha, float beta, const float* bias,
+                         void* aux, long ldaux, long sAux,
+                         const void* gate, long ldgate, long sGate, long tpf,
+                         const void* resid, long ldres, long sRes,
+                         float* colsum, void* stream) {
+  OWLK_REQUIRE(!colsum || (batch == 1 && !c_f32), "gemm: colsum needs batch 1 and a bf16 output");
+  GemmP p{};
+  p.colsum_req = colsum;
+  if (int e = gemm_dispatch(p, M, N, K, batch, A, lda, sA, a_trans, B, ldb, sB, b_trans, C, ldc, sC, c_f32, epi,
+                            alpha, beta, bias, aux, ldaux, sAux, gate, ldgate, sGate, tpf, resid, ldres, sRes, stream))
+    return e;
+  if (colsum && !p.colsum) return owlk_colsum(C, 0, M, N, ldc, colsum, stream);  // not fused by this kernel
+  return 0;
 }

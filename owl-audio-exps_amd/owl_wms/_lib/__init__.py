@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libowlk.so")
 L, I, F, P = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 
 _SIGS = {
-    "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P],
+    "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P, P],
     "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
     "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
     "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],

@@ -21,10 +21,11 @@ def _rowmajor(t, name):
 
 
 def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI_STORE, alpha=1.0, beta=0.0,
-         bias=None, aux=None, gate=None, tpf=1, resid=None):
+         bias=None, aux=None, gate=None, tpf=1, resid=None, colsum=None):
     """C[m, n] = epi(sum_k A(m, k) B(n, k)) for 2-D views.
 
     A: [M, K] (a_trans False) or [K, M] (a_trans True); B: [N, K] or [K, N] (b_trans True).
+    colsum: optional fp32 [N], += column sums of the stored bf16 C (fused into the DSILU epilogue).
     """
     _rowmajor(A, "A")
     _rowmajor(B, "B")
@@ -42,6 +43,8 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
             assert t.shape == (M, N) and t.stride(1) == 1 and t.dtype == BF16, nm
     if gate is not None:
         assert gate.dim() == 2 and gate.shape[1] == N and gate.stride(1) == 1 and gate.shape[0] * tpf >= M
+    if colsum is not None:
+        assert colsum.dtype == F32 and colsum.numel() == N and colsum.is_contiguous() and not out_f32
     tile = 64 if ((M + 127) // 128) * ((N + 127) // 128) < 512 else 128
     call("owlk_gemm", M, N, K, 1,
          ptr(A), A.stride(0), 0, int(a_trans),
@@ -51,7 +54,7 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
          ptr(aux), aux.stride(0) if aux is not None else 0, 0,
          ptr(gate), gate.stride(0) if gate is not None else 0, 0, int(tpf),
          ptr(resid), resid.stride(0) if resid is not None else 0, 0,
-         stream(), key=f"gemm<{tile},{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
+         ptr(colsum), stream(), key=f"gemm<{tile},{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
          flops=lambda: 2.0 * M * N * K)
     return out
 
@@ -76,7 +79,7 @@ def bgemm(A, B, out, *, a_trans=False, b_trans=False, epi=EPI_STORE, alpha=1.0, 
          ptr(out), out.stride(1), out.stride(0), 0,
          epi, float(alpha), float(beta), None,
          ptr(aux), aux.stride(1) if aux is not None else 0, aux.stride(0) if aux is not None else 0,
-         None, 0, 0, 1, None, 0, 0, stream())
+         None, 0, 0, 1, None, 0, 0, None, stream())
     return out
 
 

@@ -170,9 +170,9 @@ class DiTBlockFn(torch.autograd.Function):
         # ---- MLP branch
         dy2, dg2, dbf2 = K.gate_bwd(dx2, y2, gg2, tpf)
         db2 = dbf2.sum(0)
-        dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre)
+        db1 = torch.zeros(a_pre.shape[1], device=a_pre.device, dtype=torch.float32)  # colsum(dapre), fused
+        dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=db1)
         dw2 = K.gemm_wgrad(dy2, a)
-        db1 = K.colsum(dapre)
         dw1 = K.gemm_wgrad(dapre, h2)
         dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
         del dapre

@@ -96,9 +96,9 @@ class MMDiTBlockFn(torch.autograd.Function):
             # ---- MLP
             dy2, dg2, dbf2 = K.gate_bwd(douts[s], y2, ms[:, 5 * d:], ns[s])
             dW[11 + 4 * s] = dbf2.sum(0)
-            dapre = K.gemm(dy2, bf16_weight(fc2w), b_trans=True, epi=K.EPI_DSILU, aux=a_pre)
+            dW[9 + 4 * s] = torch.zeros(a_pre.shape[1], device=a_pre.device, dtype=torch.float32)
+            dapre = K.gemm(dy2, bf16_weight(fc2w), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=dW[9 + 4 * s])
             dW[10 + 4 * s] = K.gemm_wgrad(dy2, a)
-            dW[9 + 4 * s] = K.colsum(dapre)
             dW[8 + 4 * s] = K.gemm_wgrad(dapre, h2)
             dh2 = K.gemm(dapre, bf16_weight(fc1w), b_trans=True)
             del dapre, dy2

@@ -318,6 +318,20 @@ def test_gemm_splitk_weight_grad(M, N, K_):
     assert rel(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,Kd", [(16384 + 40, 1024, 1536), (512, 256, 192)])
+def test_gemm_dsilu_colsum(M, N, Kd):
+    """colsum= on the DSILU epilogue: fused in the 256^2 kernel (first case, ragged M), separate pass
+    otherwise (second case: too few tiles); equals the column sums of the stored bf16 output."""
+    k = K()
+    A, W = rnd(M, Kd, seed=80), rnd(N, Kd, scale=0.05, seed=81)
+    res = rnd(M, N, seed=82)
+    cs = torch.zeros(N, device=DEV)
+    d = k.gemm(A, W, epi=k.EPI_DSILU, aux=res, colsum=cs)
+    ref = k.gemm(A, W, epi=k.EPI_DSILU, aux=res)
+    assert torch.equal(d, ref)
+    assert rel(cs, ref.float().sum(0)) < 1e-5
+
+
 def test_gemm_splitk_workspace_alpha_beta():
     """256^2 split-K (48 tiles x 12 splits): partials + reduce give alpha AB + beta C; beta 0 never
     reads C (NaN-filled here)."""

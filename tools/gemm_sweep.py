@@ -27,9 +27,11 @@ def main():
     A, B = r(M, Kd), r(N, Kd)
     bias = torch.randn(N, device="cuda") * 0.1
     aux, res, g = r(M, N), r(M, N), r(M // 64, N)
+    cs = torch.zeros(N, device="cuda")
     cases = [("store", lambda: K.gemm(A, B)), ("store+bias", lambda: K.gemm(A, B, bias=bias)),
              ("silu", lambda: K.gemm(A, B, bias=bias, epi=K.EPI_SILU, aux=aux)),
              ("dsilu", lambda: K.gemm(A, B, epi=K.EPI_DSILU, aux=res)),
+             ("dsilu+cs", lambda: K.gemm(A, B, epi=K.EPI_DSILU, aux=res, colsum=cs)),
              ("gate_resid", lambda: K.gemm(A, B, bias=bias, epi=K.EPI_GATE_RESID, aux=aux, gate=g, tpf=64, resid=res))]
     for nm, fn in cases:
         t = timeit(fn, iters=10)
