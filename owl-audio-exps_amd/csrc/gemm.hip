@@ -16,7 +16,6 @@
 
 #include <algorithm>
 #include <cstdlib>
-#include <mutex>
 
 namespace {
 
@@ -890,30 +889,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
   }
 }
 
-// grow-only split-K workspace per device; growth drains the device before freeing the old one
-float* splitk_workspace(size_t bytes) {
-  static std::mutex mu;
-  static void* buf[64] = {};
-  static size_t cap[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  if (cap[dev] < bytes) {
-    if (buf[dev]) {
-      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-      (void)hipFree(buf[dev]);
-      buf[dev] = nullptr;
-      cap[dev] = 0;
-    }
-    if (hipMalloc(&buf[dev], bytes) != hipSuccess) {
-      buf[dev] = nullptr;
-      return nullptr;
-    }
-    cap[dev] = bytes;
-  }
-  return (float*)buf[dev];
-}
-
 // split-K factor for long reductions onto few 256^2 tiles (weight gradients, K = tokens): at one
 // workgroup per CU (128 KiB LDS) the grid runs in ceil(tiles * s / 256) rounds, so pick s to fill
 // the last round (e.g. 144 tiles: s = 4 -> 2.25 rounds, 75 % of the third idle; s = 7 -> 3.94);
@@ -985,7 +960,7 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
                          "gemm: clearing the split-K output failed");
           return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
         }
-        p.ws = splitk_workspace((size_t)nsp * M * N * sizeof(float));
+        p.ws = (float*)owlk::workspace((size_t)nsp * M * N * sizeof(float), owlk::WS_GEMM_SPLITK);
         OWLK_REQUIRE(p.ws, "gemm: split-K workspace of %ld x %ld x %ld fp32 not allocated", nsp, M, N);
         if (int e = dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s)) return e;
         const long work = M * (N / 4);

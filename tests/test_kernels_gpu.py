@@ -284,10 +284,19 @@ def test_flow_noise_mse():
     assert torch.equal(k.unpatchify(tgt, B, N, C, h, h).cpu(), tr)
 
 
-def test_colsum():
+@pytest.mark.parametrize("R,N", [(1000, 264), (98304, 1536), (7, 8), (20000, 4608)])
+def test_colsum(R, N):
+    """accumulates onto out; fp32 input too; ragged and narrow shapes."""
     k = K()
-    x = rnd(1000, 264, seed=60)
-    assert rel(k.colsum(x), x.float().sum(0)) < 1e-5
+    x = rnd(R, N, seed=60)
+    ref = x.float().sum(0)
+    out = k.colsum(x)
+    assert rel(out, ref) < 1e-5
+    base = torch.randn(N, device=DEV)
+    acc = base.clone()
+    k.colsum(x, out=acc)
+    assert rel(acc, base + ref) < 1e-5
+    assert rel(k.colsum(x.float()), ref) < 1e-5
 
 
 @pytest.mark.parametrize("shape", [(256, 768), (768, 256), (128, 128)])
