@@ -8,4 +8,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1
 timeout -k 10 400 python -u bench.py > $O/${TAG}_bench.log 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/${TAG}_profbench.log 2>&1
-find $O/${TAG}_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $O/${TAG}_kernel_stats.csv
+# rocprofv3 writes a rocpd database on this image: summarise it like --stats' kernel_stats.csv
+python tools/rocpd_stats.py $O/${TAG}_prof/run_results.db > $O/${TAG}_kernel_stats.csv
