@@ -72,7 +72,83 @@ struct DkdvCfg {
   static constexpr int TLQ = TL * QT;  // query rows per tile
 };
 
-template <int D, int QT_>
+// FULL tiles (no mask bits): the 2 QT blocks of 32 query rows x this wave's 32 keys run as a
+// software pipeline in one branch-free region, so the S / dP MFMAs of block i+1 issue while the
+// VALU turns block i's scores into P and dS (exp2, multiply, bf16 packing).  For the one-wave-
+// per-SIMD D 128 kernel, whose MFMA pipe has no partner wave to cover the softmax; at D 64 the
+// two co-resident waves already do that (+1 % measured there, so not used).
+template <class C, int QT>
+DEV void dkdv_full_pipelined(const char* tb, const float* l2, const float* dlt, const bf16x8 (&kf)[C::NS],
+                             const bf16x8 (&vf)[C::NS], f32x16 (&dk)[C::NDB], f32x16 (&dv)[C::NDB], int lane) {
+  const int h = lane >> 5;
+  constexpr int NB = 2 * QT;  // 32-row blocks per tile
+  auto chains = [&](int blk, f32x16& st, f32x16& dp) {
+    const int sq = blk >> 1, qb = blk & 1;
+    const char* lq = tb + sq * C::NSUB * SUB;
+    const char* ld = tb + (QT + sq) * C::NSUB * SUB;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int rowb = 64 * sq + 32 * qb + 8 * g4 + 4 * h;
+      const f32x4 L = *(const f32x4*)(l2 + rowb);
+      const f32x4 Dl = *(const f32x4*)(dlt + rowb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        st[4 * g4 + e] = L[e];
+        dp[4 * g4 + e] = Dl[e];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) {
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(lq + (s >> 2) * SUB, 32 * qb, s & 3, lane),
+                                                   kf[s], st, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row<SW_DUAL>(ld + (s >> 2) * SUB, 32 * qb, s & 3, lane),
+                                                   vf[s], dp, 0, 0, 0);
+    }
+  };
+  auto softmax = [&](f32x16& st, f32x16& dp, bf16x8 (&pf)[2], bf16x8 (&sf)[2]) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[r] = __builtin_amdgcn_exp2f(-st[r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] *= st[r];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      pf[s] = acc_frag(st, s);
+      sf[s] = acc_frag(dp, s);
+    }
+  };
+  auto grads = [&](int blk, const bf16x8 (&pf)[2], const bf16x8 (&sf)[2]) {
+    const int sq = blk >> 1, qb = blk & 1;
+    const char* lq = tb + sq * C::NSUB * SUB;
+    const char* ld = tb + (QT + sq) * C::NSUB * SUB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int db = 0; db < C::NDB; ++db) {
+        dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(ld + (db >> 1) * SUB, 32 * qb, s, db & 1, lane),
+                                                         pf[s], dv[db], 0, 0, 0);
+        dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr<SW_DUAL>(lq + (db >> 1) * SUB, 32 * qb, s, db & 1, lane),
+                                                         sf[s], dk[db], 0, 0, 0);
+      }
+  };
+  f32x16 sa, da, sb, db_;
+  bf16x8 pf[2], sf[2];
+  chains(0, sa, da);
+#pragma unroll
+  for (int blk = 0; blk < NB; blk += 2) {
+    chains(blk + 1, sb, db_);  // even block in (sa, da), odd block in (sb, db_)
+    softmax(sa, da, pf, sf);
+    __builtin_amdgcn_sched_barrier(0);
+    grads(blk, pf, sf);
+    __builtin_amdgcn_sched_barrier(0);
+    if (blk + 2 < NB) chains(blk + 2, sa, da);
+    softmax(sb, db_, pf, sf);
+    __builtin_amdgcn_sched_barrier(0);
+    grads(blk + 1, pf, sf);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int D, int QT_, bool PIPE = false>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) {
   using C = Cfg<D>;
   using G = DkdvCfg<D, QT_>;
@@ -220,6 +296,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
     }
     kind = __builtin_amdgcn_readfirstlane(kind);
 
+    if constexpr (PIPE) {
+      if (kind == TILE_FULL) {
+        dkdv_full_pipelined<C, QT>(tb, l2, dlt, kf, vf, dk, dv, lane);
+        kind = TILE_EMPTY;  // done
+      }
+    }
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
 #pragma unroll
@@ -475,7 +557,19 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
       else
         hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1>), grid, dim3(256), 0, s, p);
     } else {
-      hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1>), grid, dim3(256), 0, s, p);
+      // D 128 (one wave per SIMD): OWLK_DKDV128 = 0 plain, 1 pipelined FULL tiles, 2 128-row
+      // query tiles (two-slot ring, 130 KiB), 3 both (default; global 134.7 -> 99.6 ms, local
+      // 3.24 -> 2.70 ms at 20 heads x 98,304 tokens)
+      static const int v128 = getenv("OWLK_DKDV128") ? atoi(getenv("OWLK_DKDV128")) : 3;
+      const int v = p.m.window <= 0 ? v128 : (v128 & 1);
+      if (v == 3)
+        hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2, true>), grid, dim3(256), 0, s, p);
+      else if (v == 2)
+        hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2, false>), grid, dim3(256), 0, s, p);
+      else if (v == 1)
+        hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1, true>), grid, dim3(256), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1>), grid, dim3(256), 0, s, p);
     }
     if (int e = owlk::check_launch("attn_bwd_dkdv")) return e;
   }

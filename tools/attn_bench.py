@@ -1,6 +1,6 @@
 """Time the attention kernels at the dit_v4 shape (1 x 24 heads x 98,304 tokens, D 64).
 
-    python tools/attn_bench.py [--frames 1536] [--iters 5]
+    python tools/attn_bench.py [--frames 1536] [--iters 5] [--heads 20 --dim 128] [--bwd-only]
 Reports ms per launch and algorithmic TF/s (allowed pairs only).
 """
 import argparse
@@ -31,8 +31,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1536)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--heads", type=int, default=24)
+    ap.add_argument("--dim", type=int, default=64, help="head_dim (dit_v4_5B: --heads 20 --dim 128)")
+    ap.add_argument("--bwd-only", action="store_true")
     args = ap.parse_args()
-    H, D, tpf = 24, 64, 64
+    H, D, tpf = args.heads, args.dim, 64
     L = args.frames * tpf
     torch.manual_seed(0)
     qkv = torch.randn(1, L, 3 * H * D, device="cuda", dtype=torch.bfloat16)
@@ -54,8 +57,11 @@ def main():
                   _lib.ptr(delta), _lib.ptr(dq), dq.stride(1), dq.stride(0), _lib.ptr(dk), dk.stride(1),
                   dk.stride(0), _lib.ptr(dv), dv.stride(1), dv.stride(0), 1, H, L, L, D, D ** -0.5, tpf,
                   0 if window is None else window, 1, None, None, None, None, 0, _lib.stream())
-        t_f = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o, score_bound=K.qk_norm_bound(D)), args.iters)
-        t_f0 = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o), args.iters)
+        if args.bwd_only:
+            t_f = t_f0 = float("nan")
+        else:
+            t_f = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o, score_bound=K.qk_norm_bound(D)), args.iters)
+            t_f0 = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o), args.iters)
         t_kv = timeit(lambda: _lib.call("owlk_attn_bwd_dkdv", *args_b), args.iters)
         t_q = timeit(lambda: _lib.call("owlk_attn_bwd_dq", *args_b), args.iters)
         print(f"window={window}: pairs/head={pairs / H:.4e}")
