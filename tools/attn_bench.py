@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--heads", type=int, default=24)
     ap.add_argument("--dim", type=int, default=64, help="head_dim (dit_v4_5B: --heads 20 --dim 128)")
     ap.add_argument("--bwd-only", action="store_true")
+    ap.add_argument("--windows", default="none,16", help="comma list of frame windows ('none' = global)")
     args = ap.parse_args()
     H, D, tpf = args.heads, args.dim, 64
     L = args.frames * tpf
@@ -45,7 +46,7 @@ def main():
     q, k, v = qkv[:, :, :H * D], qkv[:, :, H * D:2 * H * D], qkv[:, :, 2 * H * D:]
     do = torch.randn(1, L, H * D, device="cuda", dtype=torch.bfloat16)
     dq, dk, dv = (torch.empty(1, L, H * D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
-    for window in (None, 16):
+    for window in [None if w == "none" else int(w) for w in args.windows.split(",")]:
         mask = K.FrameMask(tpf, window)
         pairs = K.mask_pairs(mask, L, L) * H
         o, lse = K.attn_fwd(q, k, v, H, D, mask)
