@@ -66,6 +66,24 @@ def test_gemm256_pingpong(K_, at, bt):
     assert rel(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("K_", [64, 192])
+@pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
+def test_gemm256_many_tiles_bf16(K_, at, bt):
+    """> 256 tiles of 256^2 with a bf16 output: 1 and 3 K-tiles, every layout, ragged M, bias and
+    the SiLU epilogue (pre-activation and activation both stored)."""
+    k = K()
+    M, N = 16384 + (0 if at else 40), 1280
+    A = rnd(K_, M, seed=17) if at else rnd(M, K_, seed=17)
+    B = rnd(K_, N, scale=0.1, seed=18) if bt else rnd(N, K_, scale=0.1, seed=18)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    y = ((A.float().T if at else A.float()) @ (B.float() if bt else B.float().T) + bias.bfloat16().float())
+    y = y.bfloat16().float()
+    assert rel(k.gemm(A, B, a_trans=at, b_trans=bt, bias=bias), y) < 5e-3
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    s = k.gemm(A, B, a_trans=at, b_trans=bt, bias=bias, epi=k.EPI_SILU, aux=aux)
+    assert rel(aux, y) < 5e-3 and rel(s, torch.nn.functional.silu(y)) < 5e-3
+
+
 def test_gemm256_epilogues():
     """fused epilogues on the 256^2 ping-pong path (dit_v4-like widths)."""
     k = K()
