@@ -1,4 +1,5 @@
 """Shared flow-matching objective pieces (gamerft.py:68-124, audiorft.py:59-93)."""
+import numpy as np
 import torch
 
 from .. import kernels as K
@@ -40,9 +41,21 @@ class InjectedNoise:
         return z.to(device=x.device, dtype=x.dtype)
 
 
-def handle_cfg(has_controls, cfg_prob, noise):
-    """gamerft.py:68-90 (the Python-level comparison syncs the host once, as in the reference)."""
+def handle_cfg(has_controls, cfg_prob, noise, frac_host=None):
+    """gamerft.py:68-90.  The Python-level comparison syncs the host, as in the reference, unless
+    the caller knows mean(has_controls) on the host (frac_host: it built the mask itself); the
+    fp32 arithmetic and the RNG draw order are the reference's either way."""
     if cfg_prob <= 0.0 or has_controls is None:
+        return has_controls
+    if frac_host is not None:
+        f32 = np.float32
+        frac = f32(frac_host)
+        pct_without = f32(1.0) - frac
+        if pct_without < f32(cfg_prob):
+            needed_frac = float((f32(cfg_prob) - pct_without) / frac)
+            b = has_controls.shape[0]
+            mask = (noise.rand_b(b, has_controls.device) <= needed_frac) & has_controls
+            has_controls = has_controls & (~mask)
         return has_controls
     frac = has_controls.float().mean()
     pct_without = 1.0 - frac

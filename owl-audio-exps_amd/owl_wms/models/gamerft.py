@@ -62,16 +62,20 @@ class GameRFT(nn.Module):
         self.core = GameRFTCore(config)
         self.noise_source = TorchNoise()
 
-    def handle_cfg(self, has_controls=None, cfg_prob=None):
-        return handle_cfg(has_controls, self.config.cfg_prob if cfg_prob is None else cfg_prob, self.noise_source)
+    def handle_cfg(self, has_controls=None, cfg_prob=None, frac_host=None):
+        return handle_cfg(has_controls, self.config.cfg_prob if cfg_prob is None else cfg_prob, self.noise_source,
+                          frac_host)
 
     def forward(self, x, mouse=None, btn=None, doc_id=None, return_dict=False, cfg_prob=None, has_controls=None):
         B, S, C, h, w = x.shape
+        frac_host = None  # mean(has_controls) when built here: no device -> host sync in handle_cfg
         if has_controls is None:
             has_controls = torch.ones(B, device=x.device, dtype=torch.bool)
+            frac_host = 1.0
         if mouse is None or btn is None:
             has_controls = torch.zeros_like(has_controls)
-        has_controls = self.handle_cfg(has_controls, cfg_prob)
+            frac_host = 0.0
+        has_controls = self.handle_cfg(has_controls, cfg_prob, frac_host)
         with torch.no_grad():
             xt, tgt, ts, z = noised_tokens(x, self.noise_source)
         pred = self.core.forward_tokens(xt.view(B, S * h * w, C), ts, mouse, btn, doc_id, has_controls)

@@ -86,15 +86,17 @@ class GameRFTAudio(nn.Module):
         self.cfg_prob = config.cfg_prob
         self.noise_source = TorchNoise()
 
-    def handle_cfg(self, has_controls=None, cfg_prob=None):
-        return handle_cfg(has_controls, self.cfg_prob if cfg_prob is None else cfg_prob, self.noise_source)
+    def handle_cfg(self, has_controls=None, cfg_prob=None, frac_host=None):
+        return handle_cfg(has_controls, self.cfg_prob if cfg_prob is None else cfg_prob, self.noise_source, frac_host)
 
     def forward(self, x, audio, mouse, btn, return_dict=False, cfg_prob=None, has_controls=None):
         B, n, C, h, w = x.shape
         Ca = audio.shape[-1]
+        frac_host = None
         if has_controls is None:
             has_controls = torch.ones(B, device=x.device, dtype=torch.bool)
-        has_controls = self.handle_cfg(has_controls, cfg_prob)
+            frac_host = 1.0
+        has_controls = self.handle_cfg(has_controls, cfg_prob, frac_host)
         with torch.no_grad():
             xt, tgt, ts, zv, at, atgt, za = noised_av(x, audio, self.noise_source)
         pv, pa = self.core.forward_tokens(xt.view(B, n * h * w, C), at.view(B, n, Ca), ts, mouse, btn, has_controls)

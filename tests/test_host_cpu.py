@@ -199,3 +199,29 @@ def test_sd3_euler_schedule():
     assert abs(dt[0].item() - (1 - 2.8125 / 2.875)) < 1e-6 and abs(dt[-1].item() - 0.1875 / 1.125) < 1e-6
     torch.testing.assert_close(get_sd3_euler(2), golden("sampler_tiny.pt")["av.dt"], atol=0, rtol=0)
     assert get_deltas([1.0, 0.5]) == [0.5, 0.5]
+
+
+@pytest.mark.parametrize("n_ctrl,b", [(8, 8), (7, 8), (1, 8), (0, 8), (3, 4)])
+def test_handle_cfg_host_fraction_matches_device_path(n_ctrl, b):
+    """handle_cfg with the mask's mean known on the host (frac_host, no device -> host sync) draws
+    the same rand(b) under the same condition and returns the same mask as the reference-order
+    tensor path (gamerft.py:68-90), for every has_controls fraction around cfg_prob."""
+    from owl_wms.models.flow import handle_cfg
+
+    class Rec:
+        def __init__(self, r):
+            self.r, self.calls = r, 0
+
+        def rand_b(self, n, device):
+            self.calls += 1
+            return self.r[:n]
+
+    r = torch.rand(b, generator=torch.Generator().manual_seed(n_ctrl))
+    hc = torch.zeros(b, dtype=torch.bool)
+    hc[:n_ctrl] = True
+    for cfg_prob in (0.1, 0.3, 0.9):
+        a, bb = Rec(r), Rec(r)
+        ref = handle_cfg(hc.clone(), cfg_prob, a)
+        got = handle_cfg(hc.clone(), cfg_prob, bb, frac_host=n_ctrl / b)
+        assert a.calls == bb.calls
+        assert torch.equal(ref, got)

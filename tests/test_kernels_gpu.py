@@ -410,3 +410,18 @@ def test_newton_schulz_padded_shapes(shape):
     y = newton_schulz_bf16(g[None].to(DEV))[0]
     ref = R.newton_schulz5(g, 5, order="epilogue")
     assert y.shape == shape and rel(y, ref) < 2e-2
+
+
+def test_single_document_cache():
+    """get_block_mask's one-document check on a device doc_id is cached per tensor object and
+    version: an in-place edit or a new tensor (even at a recycled address) is re-evaluated."""
+    from owl_wms.nn.attn import _single_document
+    d = torch.zeros(2, 8, dtype=torch.long, device=DEV)
+    assert _single_document(d, 8) and _single_document(d, 8)
+    d[1, 4:] = 1
+    assert not _single_document(d, 8)
+    assert _single_document(d, 4)
+    del d
+    e = torch.zeros(2, 8, dtype=torch.long, device=DEV)
+    e[0, 7] = 3
+    assert not _single_document(e, 8)
