@@ -30,8 +30,10 @@ int owlk_device_ok(void);
  *       4 AXPBY      C = bf16(bf16(alpha * bf16(acc)) + bf16(beta * aux))
  *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes.
  *   fp32 STORE with beta 0 or 1 and K >= 8192 onto a small output (weight gradients) splits K
- *   over workgroups; the per-split partials go to a library-owned device workspace (grown on
- *   first use, never shrunk) and one fixed-order reduce forms C, so the result is deterministic.
+ *   over workgroups.  With a caller-owned workspace of owlk_gemm_splitk_bytes(...) bytes (ws,
+ *   16-B aligned) the per-split partials go there and one fixed-order reduce forms C: the result
+ *   is deterministic.  Without it (ws null or too small) the splits combine by fp32 atomics onto
+ *   C (cleared first when beta = 0).  The library never allocates.
  *   colsum (optional, batch 1, bf16 C): colsum[n] += sum_m C[m, n] over the stored bf16 values
  *   (bias gradient of the next layer, fused into the DSILU epilogue of the 256^2 kernel; a
  *   separate column-sum pass otherwise).  Caller zeroes it. */
@@ -43,7 +45,10 @@ int owlk_gemm(long M, long N, long K, long batch,
               void* aux, long ldaux, long sAux,
               const void* gate, long ldgate, long sGate, long tpf,
               const void* resid, long ldres, long sRes,
-              float* colsum, void* stream);
+              float* colsum, void* ws, long ws_bytes, void* stream);
+/* bytes of split-K workspace owlk_gemm uses for these arguments (0: no split) */
+long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
+                            float beta);
 
 /* ---- AdaLN modulate (modulation.py:7-26 AdaLN.forward after its fc; :46-55 cond_adaln):
  *   y[t] = bf16(bf16(bf16(rms_norm(x[t])) * bf16(1 + scale[t/tpf])) + shift[t/tpf]); rstd[t] fp32 */

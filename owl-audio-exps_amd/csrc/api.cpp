@@ -3,9 +3,6 @@
 
 #include <cstdarg>
 #include <cstdio>
-#include <mutex>
-
-#include "common.hpp"
 
 namespace owlk {
 static thread_local char g_err[1024] = "";
@@ -26,30 +23,6 @@ int check_launch(const char* what) {
   return 0;
 }
 
-// Grow-only scratch per (device, slot).  Users are stream-ordered on the caller's stream; a slot
-// per user keeps two users' buffers apart.  Growth drains the device before freeing the old one.
-void* workspace(size_t bytes, int slot) {
-  static std::mutex mu;
-  static void* buf[64][WS_SLOTS] = {};
-  static size_t cap[64][WS_SLOTS] = {};
-  int dev = 0;
-  if (slot < 0 || slot >= WS_SLOTS || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  if (cap[dev][slot] < bytes) {
-    if (buf[dev][slot]) {
-      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-      (void)hipFree(buf[dev][slot]);
-      buf[dev][slot] = nullptr;
-      cap[dev][slot] = 0;
-    }
-    if (hipMalloc(&buf[dev][slot], bytes) != hipSuccess) {
-      buf[dev][slot] = nullptr;
-      return nullptr;
-    }
-    cap[dev][slot] = bytes;
-  }
-  return buf[dev][slot];
-}
 }  // namespace owlk
 
 extern "C" const char* owlk_last_error(void) { return owlk::g_err; }

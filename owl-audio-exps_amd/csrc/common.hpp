@@ -80,8 +80,6 @@ DEV bf16x8 pack8(const float* f) {
 namespace owlk {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
-enum { WS_GEMM_SPLITK = 0, WS_SLOTS = 1 };  // workspace users
-void* workspace(size_t bytes, int slot);  // api.cpp; null on failure
 }  // namespace owlk
 #define OWLK_REQUIRE(cond, ...)             \
   do {                                      \

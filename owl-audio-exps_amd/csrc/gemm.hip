@@ -912,6 +912,25 @@ long pick_splits(long tiles, long K) {
 }
 }  // namespace
 
+// The 256^2 split-K plan for an fp32 output (weight gradients): number of K splits (1 = none).
+// Shared by the launch and by owlk_gemm_splitk_bytes, so the caller sizes the workspace exactly.
+static bool fits256(long M, long N, long K, int a_trans, int b_trans, int c_f32, float beta) {
+  static const int use256 = getenv("OWLK_GEMM_NO256") ? 0 : 1;
+  return use256 && K % 64 == 0 && N % 256 == 0 && (!a_trans || M % 256 == 0) && (!b_trans || N % 256 == 0) &&
+         !(c_f32 && beta != 0.f && beta != 1.f);
+}
+static long splitk_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
+                        float beta) {
+  if (!fits256(M, N, K, a_trans, b_trans, c_f32, beta)) return 1;
+  const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
+  if (!(c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && tiles256 < 1024))
+    return 1;
+  const long splits = pick_splits(tiles256, K);
+  if (splits <= 1) return 1;
+  const long kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  return (K + kchunk - 1) / kchunk;
+}
+
 static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
                          const void* A, long lda, long sA, int a_trans,
                          const void* B, long ldb, long sB, int b_trans,
@@ -920,7 +939,7 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
                          void* aux, long ldaux, long sAux,
                          const void* gate, long ldgate, long sGate, long tpf,
                          const void* resid, long ldres, long sRes,
-                         void* stream) {
+                         void* ws, long ws_bytes, void* stream) {
   OWLK_REQUIRE(M > 0 && N > 0 && K > 0 && batch > 0, "gemm: bad sizes M=%ld N=%ld K=%ld b=%ld", M, N, K, batch);
   OWLK_REQUIRE(N % 8 == 0, "gemm: N=%ld must be a multiple of 8", N);
   OWLK_REQUIRE(a_trans ? (M % 8 == 0) : (K % 8 == 0), "gemm: A contiguous dim must be a multiple of 8");
@@ -942,26 +961,24 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   p.kchunk = K;
-  static const int use256 = getenv("OWLK_GEMM_NO256") ? 0 : 1;
-  const bool fits256 = use256 && K % 64 == 0 && N % 256 == 0 && (!a_trans || M % 256 == 0) &&
-                       (!b_trans || N % 256 == 0) && !(c_f32 && beta != 0.f && beta != 1.f);
-  if (fits256) {
-    // split-K onto an fp32 output: partials to a workspace + one reduce pass (any beta), or with
-    // OWLK_GEMM_ATOMIC=1 fp32 atomics into a caller-zeroed output (beta 1)
+  if (fits256(M, N, K, a_trans, b_trans, c_f32, beta)) {
+    // split-K onto an fp32 output: partials into the caller's workspace + one fixed-order reduce
+    // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32
+    // atomics onto C, cleared first when beta = 0
     static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
-    if (c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && tiles256 < 1024) {
+    const long nsp = splitk_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+    if (nsp > 1) {
       const long splits = pick_splits(tiles256, K);
-      if (splits > 1) {
-        p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
-        const long nsp = (K + p.kchunk - 1) / p.kchunk;
-        if (atomic_splitk) {
-          if (beta == 0.f)
-            OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
-                         "gemm: clearing the split-K output failed");
-          return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
-        }
-        p.ws = (float*)owlk::workspace((size_t)nsp * M * N * sizeof(float), owlk::WS_GEMM_SPLITK);
-        OWLK_REQUIRE(p.ws, "gemm: split-K workspace of %ld x %ld x %ld fp32 not allocated", nsp, M, N);
+      p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+      const long need = nsp * M * N * (long)sizeof(float);
+      if (atomic_splitk || !ws || ws_bytes < need || (uintptr_t)ws % 16) {
+        if (beta == 0.f)
+          OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
+                       "gemm: clearing the split-K output failed");
+        return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
+      }
+      {
+        p.ws = (float*)ws;
         if (int e = dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s)) return e;
         const long work = M * (N / 4);
         const unsigned grid = (unsigned)std::min<long>((work + 255) / 256, 2048);
@@ -1002,13 +1019,21 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
                          void* aux, long ldaux, long sAux,
                          const void* gate, long ldgate, long sGate, long tpf,
                          const void* resid, long ldres, long sRes,
-                         float* colsum, void* stream) {
+                         float* colsum, void* ws, long ws_bytes, void* stream) {
   OWLK_REQUIRE(!colsum || (batch == 1 && !c_f32), "gemm: colsum needs batch 1 and a bf16 output");
   GemmP p{};
   p.colsum_req = colsum;
   if (int e = gemm_dispatch(p, M, N, K, batch, A, lda, sA, a_trans, B, ldb, sB, b_trans, C, ldc, sC, c_f32, epi,
-                            alpha, beta, bias, aux, ldaux, sAux, gate, ldgate, sGate, tpf, resid, ldres, sRes, stream))
+                            alpha, beta, bias, aux, ldaux, sAux, gate, ldgate, sGate, tpf, resid, ldres, sRes, ws,
+                            ws_bytes, stream))
     return e;
   if (colsum && !p.colsum) return owlk_colsum(C, 0, M, N, ldc, colsum, stream);  // not fused by this kernel
   return 0;
+}
+
+extern "C" long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32,
+                                       int epi, float beta) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
+  const long nsp = splitk_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+  return nsp > 1 ? nsp * M * N * (long)sizeof(float) : 0;
 }

@@ -15,7 +15,9 @@ LIB_PATH = os.path.join(_HERE, "libowlk.so")
 L, I, F, P = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 
 _SIGS = {
-    "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P, P],
+    "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P, P, L,
+                  P],
+    "owlk_gemm_splitk_bytes": [L, L, L, L, I, I, I, I, F],
     "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
     "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
     "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],
@@ -39,6 +41,8 @@ _SIGS = {
     "owlk_ns_normalize": [P, I, L, L, L, I, P, P, P],
 }
 
+_RESTYPES = {"owlk_gemm_splitk_bytes": ctypes.c_long}  # size queries; every other entry returns an int status
+
 _lib = None
 
 
@@ -55,7 +59,7 @@ def lib():
                 continue
             fn = getattr(h, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_int
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
         h.owlk_last_error.restype = ctypes.c_char_p
         h.owlk_last_error.argtypes = []
         h.owlk_version.restype = ctypes.c_int

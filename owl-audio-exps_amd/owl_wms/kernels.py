@@ -7,7 +7,7 @@ import os
 
 import torch
 
-from ._lib import call, ptr, stream
+from ._lib import call, lib, ptr, stream
 
 BF16, F32 = torch.bfloat16, torch.float32
 
@@ -46,6 +46,13 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
     if colsum is not None:
         assert colsum.dtype == F32 and colsum.numel() == N and colsum.is_contiguous() and not out_f32
     tile = 64 if ((M + 127) // 128) * ((N + 127) // 128) < 512 else 128
+    # split-K weight gradients: the workspace for the per-split partials comes from torch's caching
+    # allocator (the library never allocates); stream order keeps it alive for the launch
+    ws, ws_bytes = None, 0
+    if out_f32 and K >= 8192:
+        ws_bytes = lib().owlk_gemm_splitk_bytes(M, N, K, 1, int(a_trans), int(b_trans), 1, epi, float(beta))
+        if ws_bytes > 0:
+            ws = torch.empty(ws_bytes, device=A.device, dtype=torch.uint8)
     call("owlk_gemm", M, N, K, 1,
          ptr(A), A.stride(0), 0, int(a_trans),
          ptr(B), B.stride(0), 0, int(b_trans),
@@ -54,7 +61,7 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
          ptr(aux), aux.stride(0) if aux is not None else 0, 0,
          ptr(gate), gate.stride(0) if gate is not None else 0, 0, int(tpf),
          ptr(resid), resid.stride(0) if resid is not None else 0, 0,
-         ptr(colsum), stream(), key=f"gemm<{tile},{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
+         ptr(colsum), ptr(ws), ws_bytes, stream(), key=f"gemm<{tile},{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
          flops=lambda: 2.0 * M * N * K)
     return out
 
@@ -79,7 +86,7 @@ def bgemm(A, B, out, *, a_trans=False, b_trans=False, epi=EPI_STORE, alpha=1.0, 
          ptr(out), out.stride(1), out.stride(0), 0,
          epi, float(alpha), float(beta), None,
          ptr(aux), aux.stride(1) if aux is not None else 0, aux.stride(0) if aux is not None else 0,
-         None, 0, 0, 1, None, 0, 0, None, stream())
+         None, 0, 0, 1, None, 0, 0, None, None, 0, stream())
     return out
 
 

@@ -225,3 +225,20 @@ def test_handle_cfg_host_fraction_matches_device_path(n_ctrl, b):
         got = handle_cfg(hc.clone(), cfg_prob, bb, frac_host=n_ctrl / b)
         assert a.calls == bb.calls
         assert torch.equal(ref, got)
+
+
+def test_gemm_splitk_workspace_query():
+    """owlk_gemm_splitk_bytes (host-only arithmetic): the split-K workspace a weight-gradient GEMM
+    needs; 0 where owlk_gemm does not split (short K, bf16 output, too many tiles)."""
+    from owl_wms._lib import LIB_PATH, lib
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("libowlk.so not built (run __graft_entry__.build())")
+    q = lib().owlk_gemm_splitk_bytes
+    # fc1 dW at dit_v4: 24 x 6 = 144 tiles of 256^2, K = 98,304 -> 7 splits (1,008 workgroups,
+    # 3.94 rounds of 256 CUs)
+    assert q(6144, 1536, 98304, 1, 1, 1, 1, 0, 0.0) == 7 * 6144 * 1536 * 4
+    assert q(6144, 1536, 98304, 1, 1, 1, 1, 0, 1.0) == 7 * 6144 * 1536 * 4
+    assert q(6144, 1536, 1536, 1, 1, 1, 1, 0, 0.0) == 0        # short K
+    assert q(6144, 1536, 98304, 1, 1, 1, 0, 0, 0.0) == 0       # bf16 output
+    assert q(98304, 6144, 98304, 1, 1, 1, 1, 0, 0.0) == 0      # enough tiles, no split
+    assert q(6144, 1536, 98304, 1, 1, 1, 1, 0, 0.5) == 0       # beta other than 0 / 1

@@ -375,6 +375,22 @@ def test_gemm_splitk_workspace_alpha_beta():
     assert rel(out, 0.5 * ref + c0) < 1e-5
 
 
+def test_gemm_splitk_without_workspace():
+    """owlk_gemm with no workspace on a split-K shape combines the splits by fp32 atomics: beta 0
+    clears C first (NaN-filled here), beta 1 accumulates."""
+    from owl_wms import _lib
+    M, N, K_ = 1536, 2048, 24576
+    dy, x = rnd(K_, M, seed=74), rnd(K_, N, seed=75)
+    ref = dy.float().T @ x.float()
+    assert _lib.lib().owlk_gemm_splitk_bytes(M, N, K_, 1, 1, 1, 1, 0, 0.0) > 0
+    for beta in (0.0, 1.0):
+        out = torch.full((M, N), float("nan"), device=DEV) if beta == 0.0 else torch.ones(M, N, device=DEV)
+        _lib.call("owlk_gemm", M, N, K_, 1, _lib.ptr(dy), dy.stride(0), 0, 1, _lib.ptr(x), x.stride(0), 0, 1,
+                  _lib.ptr(out), out.stride(0), 0, 1, 0, 1.0, beta, None, None, 0, 0, None, 0, 0, 1, None, 0, 0,
+                  None, None, 0, _lib.stream())
+        assert rel(out, ref + beta) < 1e-5
+
+
 def test_frame_mux_roundtrip():
     """frame_interleave == per-frame torch.cat (mmattn.py:54-60); frame_split is its exact inverse."""
     k = K()
