@@ -138,7 +138,8 @@ class DiTBlock(nn.Module):
         ab1, g1, ab2, g2 = self.modulation(cond)
         H = cfg.n_heads
         rope = self.attn.rope
-        geo = BlockGeometry(H, cfg.d_model // H, cfg.tokens_per_frame, block_mask, rope.cos, rope.sin, 0)
+        geo = BlockGeometry(H, cfg.d_model // H, cfg.tokens_per_frame, block_mask, rope.cos, rope.sin, 0,
+                            keep_attn=id(self) if getattr(self, "_checkpointed", False) else None)
         a, m = self.attn, self.mlp
         return DiTBlockFn.apply(x.to(torch.bfloat16).contiguous(), ab1, g1, ab2, g2, a.qkv.weight, a.qkv.bias,
                                 a.out.weight, a.out.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias, geo)
@@ -195,6 +196,7 @@ class DiT(nn.Module):
         ckpt = self.training and getattr(self.config, "gradient_checkpointing", False) and kv_cache is None
         for i, block in enumerate(self.blocks):
             mask = local_block_mask if self.local_layers[i] else global_block_mask
+            block._checkpointed = ckpt  # the re-run inside backward reuses the kept attention output
             x = checkpoint(block, x, cond, mask, kv_cache) if ckpt else block(x, cond, mask, kv_cache)
         return x
 

@@ -262,3 +262,33 @@ def test_audio_caching_sampler_vs_reference():
         out = sampler(m.core, S["audio.in.x"].cuda())
     assert out.shape == S["audio.out"].shape
     assert rel(out[:, 8:], S["audio.out"][:, 8:]) < 2e-2
+
+
+def test_checkpointed_blocks_reuse_attention():
+    """gradient_checkpointing (dit_v4_5B): the re-run of each block inside backward takes the
+    attention output kept from the first pass, so one attention forward runs per layer per step;
+    loss and every gradient equal the non-checkpointed step (the re-run is bit-exact; fp32-atomic
+    bias-gradient sums aside, hence a 1e-6 bound)."""
+    from owl_wms import _lib
+    from owl_wms.configs import model_config
+    from owl_wms.models.flow import InjectedNoise
+    from owl_wms.models.gamerft import GameRFT
+    p = "gamerft.bf16."
+    grads, losses, nfwd = [], [], []
+    for ckpt in (False, True):
+        m = det_init_(GameRFT(model_config(**TINY, gradient_checkpointing=ckpt)), base_seed=1000).cuda().train()
+        m.noise_source = InjectedNoise({"rand_b": GR[p + "in.rand_b"], "ts_raw": GR[p + "in.ts_raw"],
+                                        "z": GR[p + "in.z"]})
+        _lib.profile_begin()
+        loss = m(GR[p + "in.x"].cuda(), GR[p + "in.mouse"].cuda(), GR[p + "in.btn"].cuda(),
+                 GR[p + "in.doc_id"].cuda())
+        loss.backward()
+        prof = _lib.profile_end()
+        nfwd.append(sum(n for k, (n, _, _) in prof.items() if k.startswith("attn_fwd")))
+        losses.append(loss.item())
+        grads.append({k: q.grad.detach().clone() for k, q in m.named_parameters() if q.grad is not None})
+    assert nfwd == [TINY["n_layers"], TINY["n_layers"]]
+    assert losses[0] == losses[1]
+    assert grads[0].keys() == grads[1].keys()
+    for k in grads[0]:
+        assert rel(grads[1][k], grads[0][k]) < 1e-6, k
