@@ -1,6 +1,9 @@
-"""Data (reference: owl_wms/data/).  The real S3/NpyTable loaders are out of scope;
+"""Data (reference: owl_wms/data/).  ``sequence_packing`` over an on-disk NpyTable is in
+``latent_seq_packing`` / ``npy_table``; the S3 loaders are out of scope.
 ``synthetic`` yields batches of the configured latent shape for benchmarking and
 plumbing runs, with the reference's batch tuple layout."""
+import os
+
 import torch
 
 
@@ -33,6 +36,12 @@ class SyntheticLoader:
 
 
 def get_loader(data_id, batch_size, model_cfg=None, n_batches=10 ** 9, **kwargs):
+    """data/__init__.py:1-19.  ``sequence_packing`` with an existing ``dataset_path`` reads a real
+    NpyTable (latent_seq_packing.py); without one it falls back to synthetic latents of the shape."""
+    path = kwargs.get("dataset_path")
+    if data_id == "sequence_packing" and path and os.path.exists(os.path.join(path, "manifest.json")):
+        from . import latent_seq_packing
+        return latent_seq_packing.get_loader(batch_size, **kwargs)
     if data_id in ("synthetic", "sequence_packing", "cod", "synthetic_video"):
         return SyntheticLoader(lambda i: synthetic_video_batch(model_cfg, batch_size, seed=1234 + i,
                                                                n_docs=kwargs.get("n_docs", 1)), n_batches)

@@ -171,8 +171,10 @@ def frame_arrays(doc_id, n_frames, window, causal=True):
     # first / last occurrence of each frame's doc id (documents need not be contiguous)
     first = torch.empty_like(doc)
     last = torch.empty_like(doc)
+    dense = torch.empty_like(doc)  # ids renumbered 0..k-1 per sample, so any int64 id fits int32
     for b in range(B):
         _, inv = torch.unique(doc[b], return_inverse=True)
+        dense[b] = inv
         k = int(inv.max().item()) + 1
         fo = torch.full((k,), n_frames, device=dev, dtype=torch.int64).scatter_reduce(0, inv, idx[b], "amin")
         lo = torch.full((k,), -1, device=dev, dtype=torch.int64).scatter_reduce(0, inv, idx[b], "amax")
@@ -187,7 +189,7 @@ def frame_arrays(doc_id, n_frames, window, causal=True):
         pass  # kernels widen the kv range symmetrically from the window themselves
     i32 = torch.int32
     return {"kv_lo": kv_lo.to(i32).contiguous(), "q_hi": q_hi.to(i32).contiguous(),
-            "run_start": run_start.to(i32).contiguous(), "doc": doc.to(i32).contiguous()}
+            "run_start": run_start.to(i32).contiguous(), "doc": dense.to(i32).contiguous()}
 
 
 def _v3(t, name):

@@ -72,10 +72,13 @@ class RFTTrainer(BaseTrainer):
         return self.model(vid, mouse, btn, doc_id)
 
     def loader(self):
+        """rft_trainer.py:148-151: ``data_id`` + ``data_kwargs``.  A ``sequence_packing`` config whose
+        ``dataset_path`` holds an NpyTable reads it (packed windows with per-frame doc_id); without
+        one the loader yields synthetic latents of the configured shape."""
         kw = dict(self.train_cfg.get("data_kwargs") or {})
-        kw.pop("dataset_path", None)
-        return get_loader("synthetic", self.train_cfg.batch_size, model_cfg=self.model_cfg,
-                          n_docs=kw.get("n_docs", 1))
+        data_id = self.train_cfg.get("data_id") or "synthetic"
+        kw.setdefault("batch_columns", ["depth_latent", "mouse", "buttons"])
+        return get_loader(data_id, self.train_cfg.batch_size, model_cfg=self.model_cfg, **kw)
 
     def train(self):
         torch.cuda.set_device(self.local_rank)
@@ -84,8 +87,9 @@ class RFTTrainer(BaseTrainer):
         timer = Timer()
         timer.reset()
         local_step, loss_sum = 0, torch.zeros((), device="cuda")
+        loader = self.loader()  # built once: persistent workers survive epochs
         for epoch in range(self.train_cfg.epochs):
-            for batch in self.loader():
+            for batch in loader:
                 self.reducer.begin(sync=(local_step + 1) % accum == 0)
                 loss = self.batch_loss(batch) / accum
                 loss.backward()
