@@ -130,6 +130,23 @@ int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, v
 /* ---- Newton-Schulz (muon.py:11-38) helpers: X /= (||X||_F + eps) per batch item, bf16 */
 int owlk_ns_normalize(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
                       float* work, void* stream);
+/* the scale pass of owlk_ns_normalize alone, given sumsq[batch] = sum(bf16(g)^2) per matrix */
+int owlk_ns_scale(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
+                  const float* sumsq, void* stream);
+
+/* ---- fused Muon passes (optim.hip; replace muon.py:66-84's torch elementwise ops) ----
+ * owlk_muon_momentum: for each of `count` fp32 matrices of n elements (host array of device
+ *   pointers g[i], buf[i]): buf = lerp(buf, g, 1 - momentum); g' = nesterov ? lerp(g, buf, momentum)
+ *   : buf (muon.py:67-73).  g' goes to stack[i*n ...] (fp32, the batched NS input) or, with
+ *   stack == NULL, back into g (the reference's in-place update).  sumsq[i] += sum(bf16(g')^2)
+ *   (caller zeroes it; NULL skips), the Frobenius-norm input of owlk_ns_scale (muon.py:24-26).
+ * owlk_muon_apply: p[i] = p[i] * decay - alpha * u[i] (muon.py:80-84: decay = 1 - lr*wd,
+ *   alpha = lr * max(1, rows/cols)^0.5); u bf16 [count, rows, cols], or [count, cols, rows] with
+ *   transpose = 1 (the NS iterate before its transpose back). */
+int owlk_muon_momentum(int count, float* const* g, float* const* buf, long n, float momentum, int nesterov,
+                       float* stack, float* sumsq, void* stream);
+int owlk_muon_apply(int count, float* const* p, const void* u, long rows, long cols, int transpose, float decay,
+                    float alpha, void* stream);
 
 /* ---- MMDiT plumbing (frames.hip) ----
  * owlk_frame_mux replaces the per-frame concat / split of mmattn.py:54-60 and :77-80: frame f of

@@ -84,3 +84,24 @@ extern "C" int owlk_ns_normalize(const void* g, int g_f32, long rows, long cols,
   }
   return owlk::check_launch("ns_normalize");
 }
+
+// The scale pass alone, for callers that already hold sum(bf16(g)^2) per matrix (owlk_muon_momentum
+// accumulates it while it writes g).
+extern "C" int owlk_ns_scale(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
+                             const float* sumsq, void* stream) {
+  OWLK_REQUIRE(rows > 0 && cols > 0 && batch > 0 && sumsq && x && g, "ns_scale: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g2((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64), (unsigned)batch);
+  if (g_f32) {
+    if (transpose)
+      hipLaunchKernelGGL((scale_k<float, true>), g2, dim3(256), 0, s, (const float*)g, rows, cols, sumsq, (bf16*)x);
+    else
+      hipLaunchKernelGGL((scale_k<float, false>), g2, dim3(256), 0, s, (const float*)g, rows, cols, sumsq, (bf16*)x);
+  } else {
+    if (transpose)
+      hipLaunchKernelGGL((scale_k<bf16, true>), g2, dim3(256), 0, s, (const bf16*)g, rows, cols, sumsq, (bf16*)x);
+    else
+      hipLaunchKernelGGL((scale_k<bf16, false>), g2, dim3(256), 0, s, (const bf16*)g, rows, cols, sumsq, (bf16*)x);
+  }
+  return owlk::check_launch("ns_scale");
+}

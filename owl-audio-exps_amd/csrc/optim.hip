@@ -1,0 +1,167 @@
+// Fused Muon optimizer passes (reference muon.py:66-84), HBM-bound elementwise work.
+//
+// owlk_muon_momentum: one pass per parameter group does what the reference spends three torch
+//   passes on (buf.lerp_(g, 1-m); g.lerp_(buf, m); torch.stack) plus the Frobenius-norm reduction
+//   of the Newton-Schulz prologue (sum of bf16(g')^2, muon.py:24-26): reads g and buf, writes buf
+//   and the stacked fp32 NS input, accumulates ||bf16(g')||^2 per matrix.
+// owlk_muon_apply: p = p * (1 - lr*wd) - lr*scale * u (muon.py:80-84, two torch passes) in one,
+//   reading u straight from the NS output layout (transposed when rows > cols, 64x64 LDS tiles).
+// Each launch takes up to kMaxT same-shaped matrices as a kernel-argument pointer table (grid.y).
+#include "common.hpp"
+
+namespace {
+
+constexpr int kMaxT = 16;
+struct Ptrs {
+  float* a[kMaxT];
+  float* b[kMaxT];
+};
+
+// torch's lerp (ATen Lerp.h): weight < 0.5 ? self + w (end - self) : end - (end - self)(1 - w)
+DEV float lerp_t(float s, float e, float w) {
+  const float d = e - s;
+  return fabsf(w) < 0.5f ? s + w * d : e - d * (1.f - w);
+}
+
+DEV float momentum1(float& b, float g, float m, bool nesterov) {
+  b = lerp_t(b, g, 1.f - m);
+  return nesterov ? lerp_t(g, b, m) : b;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void muon_momentum_k(Ptrs P, long n, float m, int nesterov,
+                                                       float* __restrict__ stack, float* __restrict__ sumsq) {
+  const int z = blockIdx.y;
+  float* __restrict__ g = P.a[z];
+  float* __restrict__ buf = P.b[z];
+  float* __restrict__ out = stack ? stack + (long)z * n : g;
+  const bool nes = nesterov != 0;
+  float acc = 0.f;
+  if (VEC) {
+    const long n4 = n >> 2;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      const f32x4 gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
+      f32x4 bv = reinterpret_cast<const f32x4*>(buf)[i];
+      f32x4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float b = bv[j];
+        r[j] = momentum1(b, gv[j], m, nes);
+        bv[j] = b;
+        const float a = rb(r[j]);
+        acc += a * a;
+      }
+      reinterpret_cast<f32x4*>(buf)[i] = bv;
+      __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(out) + i);
+    }
+  } else {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+      float b = buf[i];
+      const float r = momentum1(b, g[i], m, nes);
+      buf[i] = b;
+      out[i] = r;
+      const float a = rb(r);
+      acc += a * a;
+    }
+  }
+  if (!sumsq) return;
+  acc = wave_sum(acc);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(sumsq + z, red[0] + red[1] + red[2] + red[3]);
+}
+
+// u[z] is [rows, cols] (TR = 0, contiguous) or [cols, rows] (TR = 1, the NS iterate before the
+// transpose back); p[z] is [rows, cols] fp32.
+__global__ __launch_bounds__(256) void muon_apply_flat_k(Ptrs P, const bf16* __restrict__ u, long n,
+                                                          float decay, float alpha) {
+  const int z = blockIdx.y;
+  float* __restrict__ p = P.a[z];
+  const bf16* __restrict__ uz = u + (long)z * n;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    p[i] = fmaf(-alpha, (float)uz[i], __fmul_rn(p[i], decay));
+}
+
+__global__ __launch_bounds__(256) void muon_apply_tr_k(Ptrs P, const bf16* __restrict__ u, long rows, long cols,
+                                                        float decay, float alpha) {
+  __shared__ float tile[64][65];
+  const int z = blockIdx.z;
+  float* __restrict__ p = P.a[z];
+  const bf16* __restrict__ uz = u + (long)z * rows * cols;
+  const long r0 = (long)blockIdx.y * 64, c0 = (long)blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {  // read u[c][r] along r
+    const int cc = i / 64, rr = i % 64;
+    const long r = r0 + rr, c = c0 + cc;
+    tile[rr][cc] = (r < rows && c < cols) ? (float)uz[c * rows + r] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {  // write p[r][c] along c
+    const int rr = i / 64, cc = i % 64;
+    const long r = r0 + rr, c = c0 + cc;
+    if (r < rows && c < cols) {
+      const long o = r * cols + c;
+      p[o] = fmaf(-alpha, tile[rr][cc], __fmul_rn(p[o], decay));
+    }
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+unsigned flat_blocks(long work, int count) {
+  // ~4 waves per CU over the whole launch (256 CUs), at least one block per 256 items
+  long b = (work + 255) / 256;
+  const long cap = 4096 / (count > 0 ? count : 1) + 1;
+  return (unsigned)(b < cap ? (b > 0 ? b : 1) : cap);
+}
+
+}  // namespace
+
+extern "C" int owlk_muon_momentum(int count, float* const* g, float* const* buf, long n, float momentum,
+                                  int nesterov, float* stack, float* sumsq, void* stream) {
+  OWLK_REQUIRE(count >= 0 && n > 0 && g && buf, "muon_momentum: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  for (int base = 0; base < count; base += kMaxT) {
+    const int k = count - base < kMaxT ? count - base : kMaxT;
+    Ptrs P{};
+    bool vec = (n % 4) == 0 && (!stack || aligned16(stack));
+    for (int i = 0; i < k; ++i) {
+      OWLK_REQUIRE(g[base + i] && buf[base + i], "muon_momentum: null tensor pointer");
+      P.a[i] = g[base + i];
+      P.b[i] = buf[base + i];
+      vec = vec && aligned16(P.a[i]) && aligned16(P.b[i]);
+    }
+    float* st = stack ? stack + (long)base * n : nullptr;
+    float* sq = sumsq ? sumsq + base : nullptr;
+    const dim3 grid(flat_blocks(vec ? n / 4 : n, k), (unsigned)k);
+    if (vec)
+      hipLaunchKernelGGL(muon_momentum_k<true>, grid, dim3(256), 0, s, P, n, momentum, nesterov, st, sq);
+    else
+      hipLaunchKernelGGL(muon_momentum_k<false>, grid, dim3(256), 0, s, P, n, momentum, nesterov, st, sq);
+  }
+  return owlk::check_launch("muon_momentum");
+}
+
+extern "C" int owlk_muon_apply(int count, float* const* p, const void* u, long rows, long cols, int transpose,
+                               float decay, float alpha, void* stream) {
+  OWLK_REQUIRE(count >= 0 && rows > 0 && cols > 0 && p && u, "muon_apply: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const long n = rows * cols;
+  for (int base = 0; base < count; base += kMaxT) {
+    const int k = count - base < kMaxT ? count - base : kMaxT;
+    Ptrs P{};
+    for (int i = 0; i < k; ++i) {
+      OWLK_REQUIRE(p[base + i], "muon_apply: null tensor pointer");
+      P.a[i] = p[base + i];
+    }
+    const bf16* ub = (const bf16*)u + (long)base * n;
+    if (transpose) {
+      const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64), (unsigned)k);
+      hipLaunchKernelGGL(muon_apply_tr_k, grid, dim3(256), 0, s, P, ub, rows, cols, decay, alpha);
+    } else {
+      const dim3 grid(flat_blocks(n, k), (unsigned)k);
+      hipLaunchKernelGGL(muon_apply_flat_k, grid, dim3(256), 0, s, P, ub, n, decay, alpha);
+    }
+  }
+  return owlk::check_launch("muon_apply");
+}

@@ -39,6 +39,9 @@ _SIGS = {
     "owlk_mse": [P, P, L, F, P, P, I, P],
     "owlk_colsum": [P, I, L, L, L, P, P],
     "owlk_ns_normalize": [P, I, L, L, L, I, P, P, P],
+    "owlk_ns_scale": [P, I, L, L, L, I, P, P, P],
+    "owlk_muon_momentum": [I, P, P, L, F, I, P, P, P],
+    "owlk_muon_apply": [I, P, P, L, L, I, F, F, P],
 }
 
 _RESTYPES = {"owlk_gemm_splitk_bytes": ctypes.c_long}  # size queries; every other entry returns an int status

@@ -307,6 +307,42 @@ def ns_normalize(g, transpose, work=None):
     return x
 
 
+def ns_scale(g, transpose, sumsq):
+    """owlk_ns_normalize's scale pass given sumsq[b] = sum(bf16(g)^2) (from muon_momentum)."""
+    b, r, c = g.shape
+    assert g.is_contiguous() and sumsq.dtype == F32 and sumsq.numel() == b
+    x = torch.empty((b, c, r) if transpose else (b, r, c), device=g.device, dtype=BF16)
+    call("owlk_ns_scale", ptr(g), int(g.dtype == F32), r, c, b, int(transpose), ptr(x), ptr(sumsq), stream())
+    return x
+
+
+def _ptr_array(ts):
+    import ctypes
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def muon_momentum(grads, bufs, momentum, nesterov, stack, sumsq):
+    """Fused buf.lerp_(g, 1-m); g' = lerp(g, buf, m) (or buf); stack[i] = g'; sumsq[i] += |bf16 g'|^2.
+    grads / bufs: same-numel fp32 contiguous tensors; stack fp32 [len, numel]; sumsq fp32 [len] (zeroed)."""
+    n = grads[0].numel()
+    for t in list(grads) + list(bufs):
+        assert t.dtype == F32 and t.is_contiguous() and t.numel() == n and t.is_cuda
+    assert stack.dtype == F32 and stack.is_contiguous() and stack.shape == (len(grads), n)
+    assert sumsq.dtype == F32 and sumsq.numel() == len(grads)
+    call("owlk_muon_momentum", len(grads), _ptr_array(grads), _ptr_array(bufs), n, float(momentum),
+         int(bool(nesterov)), ptr(stack), ptr(sumsq), stream())
+
+
+def muon_apply(params, u, rows, cols, transpose, decay, alpha):
+    """params[i] (fp32 [rows, cols] contiguous) = params[i] * decay - alpha * u[i]; u bf16 contiguous
+    [len, rows, cols], or [len, cols, rows] with transpose."""
+    for t in params:
+        assert t.dtype == F32 and t.is_contiguous() and t.numel() == rows * cols and t.is_cuda
+    assert u.dtype == BF16 and u.is_contiguous() and u.numel() == len(params) * rows * cols
+    call("owlk_muon_apply", len(params), _ptr_array(params), ptr(u), rows, cols, int(bool(transpose)), float(decay),
+         float(alpha), stream())
+
+
 # ---------------------------------------------------------------- MMDiT plumbing (frames.hip)
 def frame_interleave(a, b, n0, n1, out=None):
     """a [F*n0, C], b [F*n1, C] token-major -> joint [F*(n0+n1), C] (frame f = a-rows | b-rows)."""

@@ -6,6 +6,10 @@ per parameter): X = bf16(G)/(||X||_F+eps) (owlk_ns_normalize, transposed when ro
 then per iteration A = X X^T, B = b A + c A A, X = a X + B X on bf16 MFMA GEMMs whose AXPBY
 epilogue applies the scalar combination in bf16 exactly as the eager reference rounds it.
 
+Momentum + Nesterov + stacking + the Frobenius norm are one fused pass per shape group
+(owlk_muon_momentum), and decoupled weight decay + the scaled update another (owlk_muon_apply),
+reading the NS iterate in its transposed layout.
+
 Distributed (muon.py:86-115): NS work is dealt round-robin over ranks by parameter index and
 the bf16 updates are exchanged with all_gather_into_tensor (RCCL over xGMI on MI355X); every
 rank then applies every update, so replicas stay bit-identical.
@@ -21,19 +25,18 @@ from . import kernels as K
 NS_A, NS_B, NS_C = 3.4445, -4.7750, 2.0315
 
 
-def newton_schulz_bf16(G: Tensor, steps: int = 5) -> Tensor:
-    """G [b, r, c] (fp32 or bf16, on the GPU) -> bf16 [b, r, c] quintic NS orthogonalisation."""
-    assert G.dim() == 3
-    b, r, c = G.shape
-    tr = r > c
+def _pad8(G: Tensor) -> Tensor:
     # the GEMMs need dims that are multiples of 8: zero-pad (exact -- zero rows/columns add nothing
     # to ||X||_F or X X^T and stay zero through every iteration), e.g. mouse angle_proj [256, 2]
+    r, c = G.shape[-2:]
     pr, pc = (-r) % 8, (-c) % 8
-    if pr or pc:
-        G = torch.nn.functional.pad(G, (0, pc, 0, pr))
-    X = K.ns_normalize(G, tr)
-    m = X.shape[1]
-    A = torch.empty(b, m, m, device=G.device, dtype=torch.bfloat16)
+    return torch.nn.functional.pad(G, (0, pc, 0, pr)) if (pr or pc) else G
+
+
+def _ns_iterate(X: Tensor, steps: int) -> Tensor:
+    """Quintic iterations on a normalised bf16 X [b, m, k] (m <= k); returns the final iterate."""
+    b, m, _ = X.shape
+    A = torch.empty(b, m, m, device=X.device, dtype=torch.bfloat16)
     Bm = torch.empty_like(A)
     X2 = torch.empty_like(X)
     for _ in range(steps):
@@ -41,8 +44,29 @@ def newton_schulz_bf16(G: Tensor, steps: int = 5) -> Tensor:
         K.bgemm(A, A, Bm, epi=K.EPI_AXPBY, alpha=NS_C, beta=NS_B, aux=A)      # B = b A + c A A
         K.bgemm(Bm, X, X2, b_trans=True, epi=K.EPI_AXPBY, alpha=1.0, beta=NS_A, aux=X)  # X = a X + B X
         X, X2 = X2, X
+    return X
+
+
+def newton_schulz_bf16(G: Tensor, steps: int = 5) -> Tensor:
+    """G [b, r, c] (fp32 or bf16, on the GPU) -> bf16 [b, r, c] quintic NS orthogonalisation."""
+    assert G.dim() == 3
+    b, r, c = G.shape
+    tr = r > c
+    X = _ns_iterate(K.ns_normalize(_pad8(G), tr), steps)
     X = X.transpose(1, 2) if tr else X
-    return X[:, :r, :c] if (pr or pc) else X
+    return X[:, :r, :c] if X.shape[1:] != (r, c) else X
+
+
+def momentum_update(grads, bufs, momentum, nesterov, out, sumsq):
+    """muon.py:67-73 for same-numel fp32 grads, fused (owlk_muon_momentum): bufs updated in place,
+    the Nesterov-combined gradients written to out [len, numel] (not back into p.grad), sumsq[i] +=
+    ||bf16(g'_i)||^2."""
+    K.muon_momentum(grads, bufs, momentum, nesterov, out, sumsq)
+
+
+def apply_update(params, u, rows, cols, transpose, decay, alpha):
+    """muon.py:80-84 fused (owlk_muon_apply): p = p * decay - alpha * u."""
+    K.muon_apply(params, u, rows, cols, transpose, decay, alpha)
 
 
 def zeropower_via_newtonschulz5(G: Tensor, steps: int) -> Tensor:
@@ -76,20 +100,18 @@ class Muon(torch.optim.Optimizer):
             groups.append(dict(params=[p for p in params if p.numel() == size]))
         super().__init__(groups, defaults)
 
-    @torch.no_grad()
-    def _momentum(self, group, p):
-        g = p.grad
-        st = self.state[p]
-        if "momentum_buffer" not in st:
-            st["momentum_buffer"] = torch.zeros_like(g)
-        buf = st["momentum_buffer"]
-        buf.lerp_(g, 1 - group["momentum"])
-        return g.lerp_(buf, group["momentum"]) if group["nesterov"] else buf
+    def _buffers(self, params):
+        bufs = []
+        for p in params:
+            st = self.state[p]
+            if "momentum_buffer" not in st:
+                st["momentum_buffer"] = torch.zeros_like(p.grad, memory_format=torch.contiguous_format)
+            bufs.append(st["momentum_buffer"])
+        return bufs
 
-    @torch.no_grad()
-    def _apply(self, group, p, u):
-        p.mul_(1 - group["lr"] * group["weight_decay"])
-        p.add_(u.view_as(p), alpha=-group["lr"] * max(1, p.size(-2) / p.size(-1)) ** 0.5)
+    @staticmethod
+    def _scales(group, rows, cols):
+        return 1 - group["lr"] * group["weight_decay"], group["lr"] * max(1, rows / cols) ** 0.5
 
     @torch.no_grad()
     def step(self):
@@ -97,18 +119,28 @@ class Muon(torch.optim.Optimizer):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
                 continue
+            for p in params:  # the fused passes take flat fp32 storage
+                if not p.grad.is_contiguous():
+                    p.grad = p.grad.contiguous()
             if self.world_size == 1:
-                gs = [self._momentum(group, p) for p in params]
-                # batch all same-shape parameters of the group into one NS launch sequence
+                # all same-shape parameters of the group as one batch: one momentum pass (which also
+                # stacks the NS input and reduces its norm), one NS launch sequence, one apply pass
                 by_shape = {}
-                for p, g in zip(params, gs):
-                    by_shape.setdefault(tuple(g.view(len(g), -1).shape if g.ndim == 4 else g.shape), []).append(
-                        (p, g))
-                for shape, items in by_shape.items():
-                    G = torch.stack([g.reshape(shape) for _, g in items])
-                    U = newton_schulz_bf16(G, group["ns_steps"])
-                    for (p, _), u in zip(items, U):
-                        self._apply(group, p, u)
+                for p in params:
+                    by_shape.setdefault((p.grad.shape[0], p.grad[0].numel()), []).append(p)
+                for (r, c), ps in by_shape.items():
+                    G = torch.empty(len(ps), r * c, device=ps[0].device, dtype=torch.float32)
+                    sumsq = torch.zeros(len(ps), device=G.device, dtype=torch.float32)
+                    momentum_update([p.grad for p in ps], self._buffers(ps), group["momentum"], group["nesterov"],
+                                    G, sumsq)
+                    tr = r > c
+                    X = _ns_iterate(K.ns_scale(_pad8(G.view(len(ps), r, c)).contiguous(), tr, sumsq),
+                                    group["ns_steps"])
+                    if X.shape[1:] != ((c, r) if tr else (r, c)):  # zero-padded matrix: crop first
+                        X = (X.transpose(1, 2) if tr else X)[:, :r, :c].contiguous()
+                        tr = False
+                    decay, alpha = self._scales(group, r, c)
+                    apply_update(ps, X, r, c, tr, decay, alpha)
                 continue
             # multi-rank: round-robin NS + all_gather of the flat bf16 updates (muon.py:86-115)
             numel = params[0].numel()
@@ -118,14 +150,18 @@ class Muon(torch.optim.Optimizer):
                 chunk = params[base:base + ws]
                 if self.rank < len(chunk):
                     p = chunk[self.rank]
-                    g = self._momentum(group, p)
-                    g2 = g.view(len(g), -1) if g.ndim == 4 else g
-                    mine = newton_schulz_bf16(g2[None], group["ns_steps"])[0].flatten()
+                    r = p.grad.shape[0]
+                    G = torch.empty(1, numel, device=p.device, dtype=torch.float32)
+                    sumsq = torch.zeros(1, device=p.device, dtype=torch.float32)
+                    momentum_update([p.grad], self._buffers([p]), group["momentum"], group["nesterov"], G, sumsq)
+                    mine = newton_schulz_bf16(G.view(1, r, numel // r), group["ns_steps"])[0].flatten()
                 else:
                     mine = torch.zeros(numel, device=buf.device, dtype=torch.bfloat16)
                 _all_gather(buf, mine.contiguous())
                 for i, p in enumerate(chunk):
-                    self._apply(group, p, buf[i])
+                    r = p.shape[0]
+                    decay, alpha = self._scales(group, p.size(-2), p.size(-1))
+                    apply_update([p.data], buf[i], r, numel // r, False, decay, alpha)
 
 
 class CombinedOptimizer(Optimizer):

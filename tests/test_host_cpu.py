@@ -126,6 +126,18 @@ def _worker(rank, ws, port, q):
         # distributed Muon: round-robin NS + all_gather_into_tensor, NS from the CPU oracle
         import owl_wms.muon as mu
         mu.newton_schulz_bf16 = lambda G, steps=5: torch.stack([R.newton_schulz5(x, steps) for x in G])
+
+        # torch restatements of the fused HIP passes (muon.py:67-84) stand in for them on the CPU
+        def _mom(grads, bufs, m, nesterov, out, sumsq):
+            for i, (g, b) in enumerate(zip(grads, bufs)):
+                b.lerp_(g, 1 - m)
+                out[i] = (g.lerp(b, m) if nesterov else b).flatten()
+
+        def _app(params, u, r, c, tr, decay, alpha):
+            for i, p in enumerate(params):
+                p.mul_(decay).add_(u.view(len(params), r, c)[i].float(), alpha=-alpha)
+
+        mu.momentum_update, mu.apply_update = _mom, _app
         ps = [torch.nn.Parameter(torch.randn(8, 12, generator=torch.Generator().manual_seed(i))) for i in range(3)]
         for i, p in enumerate(ps):
             p.grad = torch.randn(8, 12, generator=torch.Generator().manual_seed(50 + i))

@@ -441,3 +441,81 @@ def test_single_document_cache():
     e = torch.zeros(2, 8, dtype=torch.long, device=DEV)
     e[0, 7] = 3
     assert not _single_document(e, 8)
+
+
+# ------------------------------------------------------------ fused Muon passes (optim.hip)
+def _torch_momentum(g, b, m, nesterov=True):
+    """muon.py:67-73 with torch ops (the reference's own arithmetic)."""
+    b = b.lerp(g, 1 - m)
+    return (g.lerp(b, m) if nesterov else b), b
+
+
+@pytest.mark.parametrize("count,shape,misalign", [(3, (96, 40), False), (20, (64, 24), False), (2, (33, 7), True),
+                                                  (1, (4608, 1536), False)])
+@pytest.mark.parametrize("nesterov", [True, False])
+def test_muon_momentum_fused(count, shape, misalign, nesterov):
+    """One pass = lerp + Nesterov lerp + stack + sum(bf16(g')^2), vs torch's lerp ops: fp32 within
+    1 ulp-scale (2e-7 rel) -- FMA contraction may differ from ATen's lerp -- and the norm within 1e-5.
+    misalign: grads at a 4-byte offset inside a flat bucket (the reducer's views), scalar path;
+    count 20 > 16 spans two launches."""
+    n = shape[0] * shape[1]
+    gen = torch.Generator().manual_seed(7)
+    flat = torch.randn(count * n + 1, generator=gen).to(DEV)
+    off = 1 if misalign else 0
+    grads = [flat[off + i * n: off + (i + 1) * n].view(shape) for i in range(count)]
+    bufs = [torch.randn(shape, generator=gen).to(DEV) * 0.1 for _ in range(count)]
+    exp = [_torch_momentum(g, b, 0.95, nesterov) for g, b in zip(grads, bufs)]
+    out = torch.empty(count, n, device=DEV)
+    sumsq = torch.zeros(count, device=DEV)
+    g_before = [g.clone() for g in grads]
+    K().muon_momentum(grads, bufs, 0.95, nesterov, out, sumsq)
+    torch.cuda.synchronize()
+    for i, (gp, b) in enumerate(exp):
+        torch.testing.assert_close(bufs[i], b, rtol=2e-7, atol=1e-7)
+        torch.testing.assert_close(out[i].view(shape), gp, rtol=2e-7, atol=1e-7)
+        ss = gp.bfloat16().float().pow(2).sum()
+        assert abs(sumsq[i].item() / ss.item() - 1) < 1e-5
+        assert torch.equal(grads[i], g_before[i])  # written to the stack, not into p.grad
+
+
+@pytest.mark.parametrize("rows,cols,transpose,count", [(96, 40, False, 3), (40, 96, False, 2), (200, 72, True, 3),
+                                                       (6144, 1536, True, 1), (64, 64, False, 18)])
+def test_muon_apply_fused(rows, cols, transpose, count):
+    """p = p*(1 - lr wd) - lr*s*u in one pass (muon.py:80-84) vs torch's mul_ + add_(alpha); u read
+    from the NS iterate's transposed [cols, rows] layout when transpose."""
+    gen = torch.Generator().manual_seed(9)
+    ps = [torch.randn(rows, cols, generator=gen).to(DEV) for _ in range(count)]
+    u = torch.randn(count, rows, cols, generator=gen).bfloat16().to(DEV)
+    lr, wd = 1e-3, 0.01
+    decay, alpha = 1 - lr * wd, lr * max(1, rows / cols) ** 0.5
+    exp = [p.clone().mul_(decay).add_(u[i], alpha=-alpha) for i, p in enumerate(ps)]
+    ua = u.transpose(1, 2).contiguous() if transpose else u
+    K().muon_apply(ps, ua, rows, cols, transpose, decay, alpha)
+    torch.cuda.synchronize()
+    for p, e in zip(ps, exp):
+        torch.testing.assert_close(p, e, rtol=2e-7, atol=1e-8)
+
+
+def test_muon_step_fused_matches_unfused():
+    """Muon.step on the fused passes against the same step spelled with torch ops + the
+    library NS (newton_schulz_bf16), over a group mixing shapes: [96, 64] x3, [64, 96] x2 (transposed
+    NS) and a zero-padded [256, 2]; two steps, so the momentum buffers carry over."""
+    from owl_wms.muon import Muon, newton_schulz_bf16
+    gen = torch.Generator().manual_seed(11)
+    shapes = [(96, 64)] * 3 + [(64, 96)] * 2 + [(256, 2)]
+    ps = [torch.nn.Parameter(torch.randn(s, generator=gen).to(DEV)) for s in shapes]
+    qs = [p.detach().clone() for p in ps]
+    bufs = [torch.zeros_like(q) for q in qs]
+    opt = Muon(ps, lr=1e-2, momentum=0.95, rank=0, world_size=1)
+    for step in range(2):
+        grads = [torch.randn(s, generator=gen).to(DEV) for s in shapes]
+        for p, g in zip(ps, grads):
+            p.grad = g.clone()
+        opt.step()
+        for i, (q, g) in enumerate(zip(qs, grads)):
+            gp, bufs[i] = _torch_momentum(g, bufs[i], 0.95)
+            u = newton_schulz_bf16(gp[None])[0]
+            r, c = q.shape
+            q.mul_(1 - 1e-2 * 0.01).add_(u.float(), alpha=-1e-2 * max(1, r / c) ** 0.5)
+    for p, q in zip(ps, qs):
+        assert rel(p.detach(), q) < 1e-4
