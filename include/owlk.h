@@ -147,6 +147,13 @@ int owlk_muon_momentum(int count, float* const* g, float* const* buf, long n, fl
                        float* stack, float* sumsq, void* stream);
 int owlk_muon_apply(int count, float* const* p, const void* u, long rows, long cols, int transpose, float decay,
                     float alpha, void* stream);
+/* AdamW step over `count` fp32 tensors of n[i] elements (host arrays of device pointers), in
+ * torch.optim.AdamW's order (replaces the foreach AdamW of muon.py:143-146 / rft_trainer.py):
+ * p *= 1 - lr*wd; m = lerp(m, g, 1 - beta1); v = v*beta2 + (1 - beta2) g^2;
+ * p += step_size * m / (sqrt(v) / bc2_sqrt + eps), step_size = -lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t). */
+int owlk_adamw(int count, float* const* p, const float* const* g, float* const* m, float* const* v, const long* n,
+               float lr, float beta1, float beta2, float weight_decay, float eps, float step_size, float bc2_sqrt,
+               void* stream);
 
 /* ---- MMDiT plumbing (frames.hip) ----
  * owlk_frame_mux replaces the per-frame concat / split of mmattn.py:54-60 and :77-80: frame f of

@@ -106,6 +106,68 @@ __global__ __launch_bounds__(256) void muon_apply_tr_k(Ptrs P, const bf16* __res
   }
 }
 
+
+// AdamW (torch.optim.AdamW, foreach order; rft_trainer.py / muon.py:143-146): per element
+//   p = p*(1 - lr wd); m = lerp(m, g, 1 - b1); v = v b2 + (1 - b2) g g;
+//   p = p + ss * m / (sqrt(v) / bc2s + eps)       with ss = -lr / (1 - b1^t), bc2s = sqrt(1 - b2^t)
+// One launch covers up to kMaxA tensors of any sizes (grid.y = tensor); reads p g m v, writes p m v.
+constexpr int kMaxA = 16;
+struct AdamPtrs {
+  float* p[kMaxA];
+  const float* g[kMaxA];
+  float* m[kMaxA];
+  float* v[kMaxA];
+  long n[kMaxA];
+};
+
+DEV void adamw1(float& p, float g, float& m, float& v, float decay, float b1, float b2, float ss, float bc2s,
+                float eps) {
+  p = __fmul_rn(p, decay);
+  m = lerp_t(m, g, 1.f - b1);
+  v = __fadd_rn(__fmul_rn(v, b2), (1.f - b2) * g * g);
+  const float d = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), eps);
+  p = p + ss * __fdiv_rn(m, d);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void adamw_k(AdamPtrs A, float decay, float b1, float b2, float ss, float bc2s,
+                                               float eps) {
+  const int z = blockIdx.y;
+  float* __restrict__ p = A.p[z];
+  const float* __restrict__ g = A.g[z];
+  float* __restrict__ m = A.m[z];
+  float* __restrict__ v = A.v[z];
+  const long n = A.n[z];
+  if (VEC) {
+    const long n4 = n >> 2;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      f32x4 pv = reinterpret_cast<const f32x4*>(p)[i];
+      const f32x4 gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
+      f32x4 mv = reinterpret_cast<const f32x4*>(m)[i];
+      f32x4 vv = reinterpret_cast<const f32x4*>(v)[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pj = pv[j], mj = mv[j], vj = vv[j];
+        adamw1(pj, gv[j], mj, vj, decay, b1, b2, ss, bc2s, eps);
+        pv[j] = pj;
+        mv[j] = mj;
+        vv[j] = vj;
+      }
+      reinterpret_cast<f32x4*>(p)[i] = pv;
+      reinterpret_cast<f32x4*>(m)[i] = mv;
+      reinterpret_cast<f32x4*>(v)[i] = vv;
+    }
+  } else {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+      float pj = p[i], mj = m[i], vj = v[i];
+      adamw1(pj, g[i], mj, vj, decay, b1, b2, ss, bc2s, eps);
+      p[i] = pj;
+      m[i] = mj;
+      v[i] = vj;
+    }
+  }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 unsigned flat_blocks(long work, int count) {
@@ -164,4 +226,35 @@ extern "C" int owlk_muon_apply(int count, float* const* p, const void* u, long r
     }
   }
   return owlk::check_launch("muon_apply");
+}
+
+extern "C" int owlk_adamw(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                          const long* n, float lr, float beta1, float beta2, float weight_decay, float eps,
+                          float step_size, float bc2_sqrt, void* stream) {
+  OWLK_REQUIRE(count >= 0 && p && g && m && v && n && bc2_sqrt > 0.f, "adamw: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const float decay = 1.f - lr * weight_decay;
+  for (int base = 0; base < count; base += kMaxA) {
+    const int k = count - base < kMaxA ? count - base : kMaxA;
+    AdamPtrs A{};
+    bool vec = true;
+    long nmax = 1;
+    for (int i = 0; i < k; ++i) {
+      const int j = base + i;
+      OWLK_REQUIRE(p[j] && g[j] && m[j] && v[j] && n[j] > 0, "adamw: null tensor or empty size");
+      A.p[i] = p[j];
+      A.g[i] = g[j];
+      A.m[i] = m[j];
+      A.v[i] = v[j];
+      A.n[i] = n[j];
+      vec = vec && (n[j] % 4) == 0 && aligned16(p[j]) && aligned16(g[j]) && aligned16(m[j]) && aligned16(v[j]);
+      nmax = n[j] > nmax ? n[j] : nmax;
+    }
+    const dim3 grid(flat_blocks(vec ? nmax / 4 : nmax, k), (unsigned)k);
+    if (vec)
+      hipLaunchKernelGGL(adamw_k<true>, grid, dim3(256), 0, s, A, decay, beta1, beta2, step_size, bc2_sqrt, eps);
+    else
+      hipLaunchKernelGGL(adamw_k<false>, grid, dim3(256), 0, s, A, decay, beta1, beta2, step_size, bc2_sqrt, eps);
+  }
+  return owlk::check_launch("adamw");
 }

@@ -343,6 +343,22 @@ def muon_apply(params, u, rows, cols, transpose, decay, alpha):
          float(alpha), stream())
 
 
+def adamw(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, weight_decay, eps, step):
+    """One torch.optim.AdamW step (same order and state) over fp32 contiguous tensors, fused."""
+    import ctypes
+    for ts in (params, grads, exp_avgs, exp_avg_sqs):
+        assert len(ts) == len(params)
+        for t in ts:
+            assert t.dtype == F32 and t.is_contiguous() and t.is_cuda
+    ns = [t.numel() for t in params]
+    assert [t.numel() for t in grads] == ns == [t.numel() for t in exp_avgs] == [t.numel() for t in exp_avg_sqs]
+    step_size = -lr / (1 - beta1 ** step)
+    bc2s = (1 - beta2 ** step) ** 0.5
+    call("owlk_adamw", len(params), _ptr_array(params), _ptr_array(grads), _ptr_array(exp_avgs),
+         _ptr_array(exp_avg_sqs), (ctypes.c_long * len(ns))(*ns), float(lr), float(beta1), float(beta2),
+         float(weight_decay), float(eps), float(step_size), float(bc2s), stream())
+
+
 # ---------------------------------------------------------------- MMDiT plumbing (frames.hip)
 def frame_interleave(a, b, n0, n1, out=None):
     """a [F*n0, C], b [F*n1, C] token-major -> joint [F*(n0+n1), C] (frame f = a-rows | b-rows)."""

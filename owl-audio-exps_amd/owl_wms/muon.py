@@ -164,6 +164,45 @@ class Muon(torch.optim.Optimizer):
                     apply_update([p.data], buf[i], r, numel // r, False, decay, alpha)
 
 
+class FusedAdamW(AdamW):
+    """torch.optim.AdamW with the step in one libowlk pass (owlk_adamw): same
+    hyper-parameters, same per-parameter state ('step', 'exp_avg', 'exp_avg_sq') and state_dict, so
+    reference checkpoints load; same arithmetic order as torch's foreach implementation."""
+
+    def __init__(self, params, **kw):
+        super().__init__(params, **kw)
+        for g in self.param_groups:
+            if g["amsgrad"] or g["maximize"] or g.get("capturable") or g.get("differentiable"):
+                raise NotImplementedError("FusedAdamW: amsgrad / maximize / capturable / differentiable")
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            by_step = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdamW does not support sparse gradients")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                by_step.setdefault(float(st["step"]), []).append(p)
+            b1, b2 = group["betas"]
+            for t, ps in by_step.items():
+                grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in ps]
+                K.adamw(ps, grads, [self.state[p]["exp_avg"] for p in ps], [self.state[p]["exp_avg_sq"] for p in ps],
+                        group["lr"], b1, b2, group["weight_decay"], group["eps"], t)
+        return loss
+
+
 class CombinedOptimizer(Optimizer):
     """muon.py:117-176: AdamW for names containing an adamw_key or ndim < 2, Muon for the rest."""
 
@@ -177,7 +216,7 @@ class CombinedOptimizer(Optimizer):
         names = list(named)
         for key in adamw_keys:
             assert any(key in n for n in names), f"AdamW key '{key}' not found in model parameters" + str(names)
-        self.adamw = AdamW(adamw_params, lr=kwargs.get("adamw_lr"), betas=tuple(kwargs.get("adamw_betas", (0.9, 0.999))),
+        self.adamw = FusedAdamW(adamw_params, lr=kwargs.get("adamw_lr"), betas=tuple(kwargs.get("adamw_betas", (0.9, 0.999))),
                            weight_decay=kwargs.get("adamw_wd", 0.01), eps=kwargs.get("adamw_eps", 1.0e-15))
         # reference defect kept on purpose: Muon's weight decay is never forwarded
         self.muon = Muon(muon_params, lr=kwargs.get("lr"), momentum=kwargs.get("momentum"), rank=rank,

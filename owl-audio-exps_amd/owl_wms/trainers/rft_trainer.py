@@ -14,7 +14,7 @@ import torch.distributed as dist
 
 from ..data import get_loader
 from ..models import get_model_cls
-from ..muon import init_muon
+from ..muon import FusedAdamW, init_muon
 from ..utils import Timer, strip_prefixes
 from ..utils.grad_reducer import EMA, GradReducer
 from .base import BaseTrainer
@@ -60,7 +60,8 @@ class RFTTrainer(BaseTrainer):
         else:
             if "betas" in opt_kwargs:
                 opt_kwargs["betas"] = tuple(opt_kwargs["betas"])
-            self.opt = getattr(torch.optim, self.train_cfg.opt)(self.model.parameters(), **opt_kwargs)
+            cls = FusedAdamW if self.train_cfg.opt == "AdamW" else getattr(torch.optim, self.train_cfg.opt)
+            self.opt = cls(self.model.parameters(), **opt_kwargs)
         self.reducer = GradReducer(self.model.parameters(), world_size=self.world_size)
         if ckpt:
             self.ema.load_state_dict(state["ema"])

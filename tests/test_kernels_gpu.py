@@ -519,3 +519,33 @@ def test_muon_step_fused_matches_unfused():
             q.mul_(1 - 1e-2 * 0.01).add_(u.float(), alpha=-1e-2 * max(1, r / c) ** 0.5)
     for p, q in zip(ps, qs):
         assert rel(p.detach(), q) < 1e-4
+
+
+@pytest.mark.parametrize("eps,wd", [(1e-15, 1e-4), (1e-8, 0.01)])
+def test_fused_adamw_matches_torch(eps, wd):
+    """FusedAdamW (owlk_adamw) vs torch.optim.AdamW (foreach) over 3 steps on 20 tensors of mixed sizes
+    (two launches of <= 16; a misaligned / odd-sized one takes the scalar path): params and both
+    moments within 1e-6 relative; state_dict keys and 'step' identical."""
+    from owl_wms.muon import FusedAdamW
+    gen = torch.Generator().manual_seed(21)
+    shapes = [(3072, 1536), (1536,), (7,), (128, 11)] + [(64, 64)] * 16
+    ps = [torch.nn.Parameter(torch.randn(s, generator=gen).to(DEV)) for s in shapes]
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    kw = dict(lr=1e-3, betas=(0.9, 0.95), weight_decay=wd, eps=eps)
+    fo, to = FusedAdamW(ps, **kw), torch.optim.AdamW(qs, foreach=True, **kw)
+    for step in range(3):
+        for p, q in zip(ps, qs):
+            g = torch.randn(p.shape, generator=gen).to(DEV) * 1e-2
+            p.grad, q.grad = g.clone(), g.clone()
+        fo.step()
+        to.step()
+    torch.cuda.synchronize()
+    for p, q in zip(ps, qs):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+        for k in ("exp_avg", "exp_avg_sq"):
+            # lerp near zero cancels: compare at 1e-6 of the moment's magnitude (FMA contraction
+            # in ATen's foreach kernels vs ours differs by an operand ulp)
+            ref = to.state[q][k]
+            torch.testing.assert_close(fo.state[p][k], ref, rtol=1e-6, atol=1e-6 * ref.abs().max().item())
+        assert float(fo.state[p]["step"]) == float(to.state[q]["step"]) == 3.0
+    assert fo.state_dict()["param_groups"][0].keys() == to.state_dict()["param_groups"][0].keys()

@@ -142,7 +142,8 @@ def test_audio_config1_trajectory():
                        tokens_per_frame=1, n_frames=10000, cfg_prob=0.0, causal=True, uncond=True, backbone="dit",
                        has_audio=True, rope_impl="audio1d", local_window=16, global_window=None)
     m = det_init_(AudioRFT(cfg), base_seed=3000).cuda().train()
-    opt = torch.optim.AdamW(m.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=0.01, eps=1e-8)
+    from owl_wms.muon import FusedAdamW  # the trainer's AdamW (owlk_adamw)
+    opt = FusedAdamW(m.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=0.01, eps=1e-8)
     for step in range(10):
         m.noise_source = InjectedNoise({"ts_raw": det_tensor((1, 120), 3200 + step),
                                         "z": det_tensor((1, 120, 64), 3300 + step)})
