@@ -18,6 +18,17 @@ class SinCosEmbed(nn.Module):
         super().__init__()
         self.dim, self.theta, self.mult = dim, theta, mult
 
+    def _freqs(self, device, dtype):
+        """exp(-i ln(theta) / (half - 1)), built on the CPU in fp32 as the reference does, then cached
+        per (device, dtype): no host-to-device copy per call (the decode loop is graph-captured)."""
+        key = (str(device), dtype)
+        cache = self.__dict__.setdefault("_freq_cache", {})
+        if key not in cache:
+            half = self.dim // 2
+            e = torch.log(torch.tensor(self.theta)) / (half - 1)
+            cache[key] = torch.exp(torch.arange(half) * -e).to(device=device, dtype=dtype)
+        return cache[key]
+
     def forward(self, x):
         if isinstance(x, float):
             x = torch.tensor([x])
@@ -30,9 +41,7 @@ class SinCosEmbed(nn.Module):
             b, n = x.shape
             x = x.reshape(b * n)
         x = x * self.mult
-        half = self.dim // 2
-        e = torch.log(torch.tensor(self.theta)) / (half - 1)
-        e = torch.exp(torch.arange(half) * -e).to(device=x.device, dtype=x.dtype)
+        e = self._freqs(x.device, x.dtype)
         e = x.unsqueeze(-1) * e.unsqueeze(0)
         e = torch.cat((torch.sin(e), torch.cos(e)), dim=-1)
         return e.reshape(b, n, -1) if reshape_out else e

@@ -21,11 +21,49 @@ class AVCachingSamplerV2:
         self.noise_prev = noise_prev
         self.max_window = max_window
         self.custom_schedule = custom_schedule
+        self._pool = None  # graph memory pool shared by the per-frame captures (compile_on_decode)
 
     @staticmethod
     def zlerp(x, alpha):
         z = torch.randn_like(x)
         return x * (1.0 - alpha) + z * alpha
+
+    def _euler_step(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
+        """av_caching_v2.py:96-110: one Euler step with optional CFG."""
+        pred_v = model(x, t, mouse, btn, kv_cache=kv_cache)
+        if self.cfg_scale != 1.0:
+            pred_u = model(x, t, null_mouse, null_btn, kv_cache=kv_cache)
+            pred_v = pred_u + self.cfg_scale * (pred_v - pred_u)
+        return x - dt * pred_v, t - dt
+
+    def _euler_graphed(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
+        """The frame's n_steps Euler steps with steps 1.. replayed from one HIP graph.
+
+        The cache is read-only and fixed in length while a frame is denoised, so every step launches
+        the same kernels on the same buffers: step 0 runs eagerly (it also warms the per-weight bf16
+        caches), one step is captured with x, t and dt in static device buffers, and the graph is
+        replayed for the remaining steps -- same kernels and arithmetic as the eager loop
+        (the reference's ``compile_on_decode`` switch)."""
+        x, t = self._euler_step(model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt[0])
+        if self.n_steps == 1:
+            return x, t
+        sx, st, sdt = x.clone(), t.clone(), dt[1].clone()
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, pool=self._pool, stream=side):
+                nx, nt = self._euler_step(model, kv_cache, sx, st, mouse, btn, null_mouse, null_btn, sdt)
+                sx.copy_(nx)
+                st.copy_(nt)
+        torch.cuda.current_stream().wait_stream(side)
+        for t_idx in range(1, self.n_steps):
+            sdt.copy_(dt[t_idx])
+            g.replay()
+        del g
+        return sx.clone(), st.clone()
 
     @torch.no_grad()
     def __call__(self, model, x, mouse, btn, compile_on_decode=False):
@@ -55,13 +93,13 @@ class AVCachingSamplerV2:
                 start = init_len + idx
                 curr_mouse, curr_btn = mouse[:, start:start + 1], btn[:, start:start + 1]
                 null_mouse, null_btn = torch.zeros_like(curr_mouse), torch.zeros_like(curr_btn)
-                for t_idx in range(self.n_steps):
-                    pred_v = model(curr_x, curr_t, curr_mouse, curr_btn, kv_cache=kv_cache).clone()
-                    if self.cfg_scale != 1.0:
-                        pred_u = model(curr_x, curr_t, null_mouse, null_btn, kv_cache=kv_cache).clone()
-                        pred_v = pred_u + self.cfg_scale * (pred_v - pred_u)
-                    curr_x = curr_x - dt[t_idx] * pred_v
-                    curr_t = curr_t - dt[t_idx]
+                if compile_on_decode:
+                    curr_x, curr_t = self._euler_graphed(model, kv_cache, curr_x, curr_t, curr_mouse, curr_btn,
+                                                         null_mouse, null_btn, dt)
+                else:
+                    for t_idx in range(self.n_steps):
+                        curr_x, curr_t = self._euler_step(model, kv_cache, curr_x, curr_t, curr_mouse, curr_btn,
+                                                          null_mouse, null_btn, dt[t_idx])
                 latents.append(curr_x.clone())
                 curr_x_noisy = self.zlerp(curr_x, self.noise_prev)
                 curr_t_noisy = torch.ones_like(curr_t) * self.noise_prev
