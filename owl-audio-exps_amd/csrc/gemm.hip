@@ -364,6 +364,18 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
     }
   __syncthreads();
 
+  if (p.ws) {
+    // skinny split-K: raw fp32 partial tile to ws[split][M][N]; splitk_epi_k sums the splits in
+    // order and applies the epilogue
+    float* W = p.ws + (long)blockIdx.y * p.M * p.N;
+    for (int c = threadIdx.x; c < BM * BN / 4; c += NT) {
+      const int row = c / (BN / 4), col = (c % (BN / 4)) * 4;
+      const long gm = m0 + row, gn = n0 + col;
+      if (gm < p.M && gn < p.N)
+        __builtin_nontemporal_store(*(const f32x4*)(ct + row * EPI_LD + col), (f32x4*)(W + gm * p.N + gn));
+    }
+    return;
+  }
   if (OF32 && EPI == EPI_STORE && gridDim.y > 1) {
     // split-K partial: each wave-instruction adds 64 consecutive floats (256 B, full atomic rate)
     float* C = (float*)p.C + z * p.sC;
@@ -889,6 +901,36 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
   }
 }
 
+// skinny split-K reduce: v = sum_s W[s][m, n .. n + 8) in split order, then the GEMM's own
+// epilogue (bias, SiLU + aux, gate + residual) on the bf16 output
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_epi_k(GemmP p, int splits) {
+  const long n8 = p.N / 8, total = p.M * n8, MN = p.M * p.N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long m = i / n8, n = (i - m * n8) * 8;
+    const float* w = p.ws + m * p.N + n;
+    float v[8];
+    {
+      const f32x4 lo = __builtin_nontemporal_load((const f32x4*)w), hi = __builtin_nontemporal_load((const f32x4*)(w + 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e];
+        v[e + 4] = hi[e];
+      }
+    }
+    for (int sp = 1; sp < splits; ++sp) {
+      const f32x4 lo = __builtin_nontemporal_load((const f32x4*)(w + sp * MN));
+      const f32x4 hi = __builtin_nontemporal_load((const f32x4*)(w + sp * MN + 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += lo[e];
+        v[e + 4] += hi[e];
+      }
+    }
+    epi_chunk<EPI, false>(p, 0, m, n, v);
+  }
+}
+
 // split-K factor for long reductions onto few 256^2 tiles (weight gradients, K = tokens): at one
 // workgroup per CU (128 KiB LDS) the grid runs in ceil(tiles * s / 256) rounds, so pick s to fill
 // the last round (e.g. 144 tiles: s = 4 -> 2.25 rounds, 75 % of the third idle; s = 7 -> 3.94);
@@ -919,8 +961,26 @@ static bool fits256(long M, long N, long K, int a_trans, int b_trans, int c_f32,
   return use256 && K % 64 == 0 && N % 256 == 0 && (!a_trans || M % 256 == 0) && (!b_trans || N % 256 == 0) &&
          !(c_f32 && beta != 0.f && beta != 1.f);
 }
+// Skinny-M GEMMs (decode: one 64-token frame against the full weights) give few 64x64 tiles; split K
+// so the grid streams the weights from every CU: bf16 output with STORE (beta 0) / SILU / GATE_RESID
+// epilogues, applied after a fixed-order reduce of the fp32 partials (deterministic).
+static long skinny_splits(long M, long N, long K, long batch, int c_f32, int epi, float beta) {
+  if (batch != 1 || c_f32 || M > 256 || K < 512 || K % BK) return 1;
+  if (!(epi == EPI_SILU || epi == EPI_GATE_RESID || (epi == EPI_STORE && beta == 0.f))) return 1;
+  const long tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  if (tiles >= 256) return 1;
+  long sp = (768 + tiles - 1) / tiles;         // ~3 workgroups per CU
+  const long maxsp = K / (2 * BK);             // >= 2 K-steps per split
+  if (sp > maxsp) sp = maxsp;
+  if (sp < 2) return 1;
+  const long kchunk = ((K + sp - 1) / sp + BK - 1) / BK * BK;
+  return (K + kchunk - 1) / kchunk;
+}
+
 static long splitk_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                         float beta) {
+  const long sk = skinny_splits(M, N, K, batch, c_f32, epi, beta);
+  if (sk > 1) return sk;
   if (!fits256(M, N, K, a_trans, b_trans, c_f32, beta)) return 1;
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   if (!(c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && tiles256 < 1024))
@@ -961,6 +1021,22 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   p.kchunk = K;
+  {
+    const long sk = skinny_splits(M, N, K, batch, c_f32, epi, beta);
+    if (sk > 1 && ws && ws_bytes >= sk * M * N * (long)sizeof(float) && (uintptr_t)ws % 16 == 0) {
+      p.kchunk = ((K + sk - 1) / sk + BK - 1) / BK * BK;
+      p.ws = (float*)ws;
+      if (int e = dispatch_e<64, 64>(p, a_trans, b_trans, epi, c_f32, batch, s)) return e;
+      const long work = M * (N / 8);
+      const unsigned grid = (unsigned)std::min<long>((work + 255) / 256, 2048);
+      switch (epi) {
+        case EPI_STORE: hipLaunchKernelGGL(splitk_epi_k<EPI_STORE>, dim3(grid), dim3(256), 0, s, p, (int)sk); break;
+        case EPI_SILU: hipLaunchKernelGGL(splitk_epi_k<EPI_SILU>, dim3(grid), dim3(256), 0, s, p, (int)sk); break;
+        default: hipLaunchKernelGGL(splitk_epi_k<EPI_GATE_RESID>, dim3(grid), dim3(256), 0, s, p, (int)sk); break;
+      }
+      return owlk::check_launch("splitk_epi");
+    }
+  }
   if (fits256(M, N, K, a_trans, b_trans, c_f32, beta)) {
     // split-K onto an fp32 output: partials into the caller's workspace + one fixed-order reduce
     // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32

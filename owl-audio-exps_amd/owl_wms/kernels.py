@@ -49,8 +49,9 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
     # split-K weight gradients: the workspace for the per-split partials comes from torch's caching
     # allocator (the library never allocates); stream order keeps it alive for the launch
     ws, ws_bytes = None, 0
-    if out_f32 and K >= 8192:
-        ws_bytes = lib().owlk_gemm_splitk_bytes(M, N, K, 1, int(a_trans), int(b_trans), 1, epi, float(beta))
+    if (out_f32 and K >= 8192) or (M <= 256 and K >= 512 and not out_f32):  # dW / skinny-M (decode) split-K
+        ws_bytes = lib().owlk_gemm_splitk_bytes(M, N, K, 1, int(a_trans), int(b_trans), int(out_f32), epi,
+                                                float(beta))
         if ws_bytes > 0:
             ws = torch.empty(ws_bytes, device=A.device, dtype=torch.uint8)
     call("owlk_gemm", M, N, K, 1,

@@ -549,3 +549,30 @@ def test_fused_adamw_matches_torch(eps, wd):
             torch.testing.assert_close(fo.state[p][k], ref, rtol=1e-6, atol=1e-6 * ref.abs().max().item())
         assert float(fo.state[p]["step"]) == float(to.state[q]["step"]) == 3.0
     assert fo.state_dict()["param_groups"][0].keys() == to.state_dict()["param_groups"][0].keys()
+
+
+@pytest.mark.parametrize("M,N,Kd", [(64, 6144, 1536), (64, 1536, 6144), (128, 4608, 1536), (72, 256, 512)])
+def test_gemm_skinny_splitk_epilogues(M, N, Kd):
+    """Skinny-M GEMMs (decode: one 64-token frame) split K over the workspace and apply the epilogue
+    after a fixed-order reduce: store + bias, SiLU + aux, gate + residual vs fp32 torch (bf16 output
+    tolerance 5e-3), deterministic across runs, and the same numbers as the unsplit path up to fp32
+    summation order."""
+    k = K()
+    from owl_wms._lib import lib
+    assert lib().owlk_gemm_splitk_bytes(M, N, Kd, 1, 0, 0, 0, k.EPI_SILU, 0.0) > 0  # the split path is taken
+    tpf = 64 if M % 64 == 0 else M
+    A, W = rnd(M, Kd, seed=13), rnd(N, Kd, scale=0.05, seed=14)
+    bias = (torch.randn(N) * 0.1).to(DEV)
+    acc = A.float() @ W.float().T
+    y = (acc + bias.bfloat16().float()).bfloat16().float()
+    o1 = k.gemm(A, W, bias=bias)
+    assert rel(o1, y) < 5e-3
+    assert torch.equal(o1, k.gemm(A, W, bias=bias))
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    s = k.gemm(A, W, bias=bias, epi=k.EPI_SILU, aux=aux)
+    assert rel(aux, y) < 5e-3 and rel(s, torch.nn.functional.silu(y)) < 5e-3
+    g = rnd((M + tpf - 1) // tpf, N, seed=15)
+    res = rnd(M, N, seed=16)
+    o = k.gemm(A, W, bias=bias, epi=k.EPI_GATE_RESID, gate=g, tpf=tpf, resid=res)
+    gref = g.float().repeat_interleave(tpf, 0)[:M]
+    assert rel(o, res.float() + gref * y) < 5e-3
