@@ -31,7 +31,7 @@ PEAK_HBM = 8.0e12
 FLOP_PER_TOKEN = 6.596e9     # dit_v4 fwd+bwd algorithmic FLOPs per token; see flops_per_token
 
 
-def flops_per_token(mc, tokens):
+def flops_per_token(mc, tokens, doc_id=None):
     """SURVEY §8(d) counting for any DiT config: 3 x (token GEMMs 24 d^2 per layer + attention 4 d x
     allowed pairs / T + proj_in/out + per-frame modulation/embedding GEMMs / tpf) -- fwd+bwd, no
     recompute, no masked pairs.  Gives 6.601e9 for dit_v4 and 3.161e10 for dit_v4_5B (SURVEY:
@@ -44,7 +44,8 @@ def flops_per_token(mc, tokens):
     for i in range(L):
         local = i % 4 != 0
         w = mc.local_window if local else getattr(mc, "global_window", None)
-        attn += 4 * d * K.mask_pairs(K.FrameMask(tpf, w), tokens, tokens) / tokens
+        arrays = None if doc_id is None else K.frame_arrays(doc_id, tokens // tpf, w)
+        attn += 4 * d * K.mask_pairs(K.FrameMask(tpf, w, arrays=arrays), tokens, tokens) / tokens
     return 3 * (gemm + per_frame + attn)
 
 
@@ -94,6 +95,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-batch", type=int, default=16)
     ap.add_argument("--frames", type=int, default=None, help="override n_frames (default: the config's)")
+    ap.add_argument("--docs", type=int, default=1,
+                    help="documents per packed sample (SURVEY §8(d) doc-mask variant: 4 x 384 frames)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--config", default="configs/dit_v4.yml",
@@ -116,7 +119,7 @@ def main():
 
     cfg = Config.from_yaml(os.path.join(REPO, args.config))
     cfg_name = os.path.splitext(os.path.basename(args.config))[0]
-    headline = cfg_name == "dit_v4"
+    headline = cfg_name == "dit_v4" and args.docs == 1
     mc = cfg.model
     if args.frames:
         mc.n_frames = args.frames
@@ -125,7 +128,8 @@ def main():
     accum = max(1, args.global_batch // world)
     torch.manual_seed(0)
     model = get_model_cls(mc.model_id)(mc).cuda().train()
-    fpt = flops_per_token(mc, tokens)
+    docs_fl = None if args.docs == 1 else (torch.arange(mc.n_frames) * args.docs // mc.n_frames)[None]
+    fpt = flops_per_token(mc, tokens, docs_fl)  # doc-masked pairs counted exactly for --docs > 1
     n_params = sum(p.numel() for p in model.parameters())
     if world > 1:
         with torch.no_grad():
@@ -136,7 +140,7 @@ def main():
     red = GradReducer(model.parameters(), world_size=world)
     batches = []
     for i in range(2):
-        b = [t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234 + rank * 97 + i)]
+        b = [t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234 + rank * 97 + i, n_docs=args.docs)]
         if av:
             g = torch.Generator().manual_seed(4321 + rank * 97 + i)
             b.append(torch.randn(1, mc.n_frames, mc.audio_channels, generator=g).to(torch.bfloat16).cuda())
@@ -242,7 +246,8 @@ def main():
                                       f"RCCL grad all-reduce + Muon/AdamW step + EMA",
                           "model": f"{cfg_name} ({mc.n_layers} L, d{mc.d_model}, {mc.n_heads} H, "
                                    f"{n_params / 1e6:.1f}M params)", "global_batch": args.global_batch,
-                          "seq_len": tokens, "parallelism": f"dp{world}"},
+                          "seq_len": tokens, "parallelism": f"dp{world}",
+                          **({"docs_per_sample": args.docs} if args.docs > 1 else {})},
                "tokens_per_s_per_gpu": round(value / world, 1),
                "step_mfma_frac": round(value * (FLOP_PER_TOKEN if headline else fpt) / world / PEAK_BF16, 4),
                "roofline": roof, "cpu_baseline": cpu}

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   const bool wave_live = kw0 < p.Lkv;
   const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
   const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
-  TileRange full = full_range_q(m, wfk0, wfk1, qbeg, p.Lq, TLQ);
+  TileRange full = full_range_q(m, b, wfk0, wfk1, qbeg, p.Lq, TLQ);
   if (!wave_live || kw0 + 32 > p.Lkv) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
   const bool wave_live = r0 < p.Lq;
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, TLK);
+  TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, TLK);
   if (!wave_live) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);

@@ -32,6 +32,11 @@ DEV int frame_of(const MaskP& m, long idx) {
   return m.magic ? (int)__umulhi((unsigned)idx, m.magic) : (int)idx;
 }
 
+// Packed documents (every doc one contiguous run of frames, causal): the caller passes kv_lo / q_hi
+// without doc / run_start.  Then allowed(q, k) <=> kv_lo[fq] <= fk <= fq (kv_lo = max(run start,
+// fq - W + 1), non-decreasing in fq) -- an index range per row, like the doc-free mask.
+DEV bool runs_mode(const MaskP& m) { return !m.doc && m.kv_lo && m.causal; }
+
 enum TileKind { TILE_EMPTY = 0, TILE_FULL = 1, TILE_PARTIAL = 2 };
 
 // classify query frames [fq0, fq1] x kv frames [fk0, fk1] for batch b
@@ -42,6 +47,11 @@ DEV int classify(const MaskP& m, long b, int fq0, int fq1, int fk0, int fk1) {
     if (!m.causal && fk0 - fq1 >= m.window) return TILE_EMPTY;
   }
   bool pure_doc = true;
+  if (runs_mode(m)) {
+    const int* kl = m.kv_lo + b * m.fstride;
+    if (fk1 < kl[fq0]) return TILE_EMPTY;
+    pure_doc = fk0 >= kl[fq1];
+  }
   if (m.doc) {
     const int* rs = m.run_start + b * m.fstride;
     const int* dc = m.doc + b * m.fstride;
@@ -61,16 +71,18 @@ DEV int classify(const MaskP& m, long b, int fq0, int fq1, int fk0, int fk1) {
 // Tiles a wave sweeps form a contiguous index range that classify() would call FULL.  Without a
 // document mask that range is analytic, so the tile loop only classifies tiles outside it (the
 // per-tile classify is ~120 scalar instructions ahead of the first MFMA).  Half-open [lo, hi);
-// empty (lo >= hi) when documents are packed.
+// empty (lo >= hi) for non-contiguous documents; packed (contiguous-run) documents narrow it by
+// kv_lo / q_hi.
 struct TileRange {
   int lo, hi;
 };
 DEV long floordiv_(long a, long b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 // self = query frames [fq0, fq1]; swept tiles = kv rows [base + t KT, base + t KT + KT)
-DEV TileRange full_range_kv(const MaskP& m, int fq0, int fq1, long base, long Lkv, int KT) {
+DEV TileRange full_range_kv(const MaskP& m, long b, int fq0, int fq1, long base, long Lkv, int KT) {
   TileRange r{1, 0};
   if (m.doc) return r;
   long cmin = base, cmax = Lkv - KT;
+  if (runs_mode(m)) cmin = max(cmin, (long)m.kv_lo[b * m.fstride + fq1] * m.tpf);
   if (m.causal) cmax = min(cmax, (long)(fq0 + 1) * m.tpf - KT);
   if (m.window > 0) {
     cmin = max(cmin, (long)(fq1 - m.window + 1) * m.tpf);
@@ -82,10 +94,11 @@ DEV TileRange full_range_kv(const MaskP& m, int fq0, int fq1, long base, long Lk
   return r;
 }
 // self = key frames [fk0, fk1]; swept tiles = query rows [base + t TL, base + t TL + TL)
-DEV TileRange full_range_q(const MaskP& m, int fk0, int fk1, long base, long Lq, int TL) {
+DEV TileRange full_range_q(const MaskP& m, long b, int fk0, int fk1, long base, long Lq, int TL) {
   TileRange r{1, 0};
   if (m.doc) return r;
   long cmin = base, cmax = Lq - TL;
+  if (runs_mode(m)) cmax = min(cmax, ((long)m.q_hi[b * m.fstride + fk0] + 1) * m.tpf - TL);
   if (m.causal) cmin = max(cmin, (long)fk1 * m.tpf);
   if (m.window > 0) {
     cmax = min(cmax, (long)(fk0 + m.window) * m.tpf - TL);
@@ -132,6 +145,12 @@ DEV unsigned long long tile_bits(const MaskP& m, long b, long self, bool self_ok
     // than the tile's MFMAs)
     const long tpf = m.tpf, W = m.window;
     long lo = 0, hi = other_len;
+    if (runs_mode(m)) {  // packed documents: the run bounds arrive through kv_lo / q_hi
+      if (self_is_query)
+        lo = max(lo, (long)m.kv_lo[b * m.fstride + fs] * tpf);
+      else
+        hi = min(hi, ((long)m.q_hi[b * m.fstride + fs] + 1) * tpf - m.q_offset);
+    }
     if (self_is_query) {  // other = keys, frame(k) in [fs - W + 1, fs] (causal) / (fs - W, fs + W)
       if (m.causal) hi = min(hi, ((long)fs + 1) * tpf);
       if (W > 0) {

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(FwdP p) {
   const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
   const bool wave_live = r0 < p.Lq;
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, KT);
+  TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, KT);
   if (!wave_live) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_k(FwdP p) {
   const long wlast = (r0 + 63 < p.Lq ? r0 + 63 : p.Lq - 1);
   const bool wave_live = r0 < p.Lq;
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  TileRange full = full_range_kv(m, wfq0, wfq1, kv_begin, p.Lkv, KT);
+  TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, KT);
   if (!wave_live) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);

@@ -156,6 +156,8 @@ class FrameMask:
         w = 0 if self.window is None else int(self.window)
         if a is None:
             return (self.tpf, w, int(self.causal), None, None, None, None, 0)
+        if a.get("runs") and self.causal:  # packed documents: kv_lo / q_hi alone describe the mask
+            return (self.tpf, w, 1, ptr(a["kv_lo"]), ptr(a["q_hi"]), None, None, a["doc"].stride(0))
         return (self.tpf, w, int(self.causal), ptr(a["kv_lo"]), ptr(a["q_hi"]), ptr(a["run_start"]), ptr(a["doc"]),
                 a["doc"].stride(0))
 
@@ -189,7 +191,10 @@ def frame_arrays(doc_id, n_frames, window, causal=True):
     if not causal:
         pass  # kernels widen the kv range symmetrically from the window themselves
     i32 = torch.int32
-    return {"kv_lo": kv_lo.to(i32).contiguous(), "q_hi": q_hi.to(i32).contiguous(),
+    # every document one contiguous run of frames (sequence packing always gives this): the
+    # kernels then take the range form of the mask (attn_common.hpp runs_mode)
+    runs = bool((first == run_start).all())
+    return {"runs": runs, "kv_lo": kv_lo.to(i32).contiguous(), "q_hi": q_hi.to(i32).contiguous(),
             "run_start": run_start.to(i32).contiguous(), "doc": dense.to(i32).contiguous()}
 
 
@@ -246,12 +251,22 @@ def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
 
 
 def mask_pairs(mask, Lq, Lkv):
-    """Allowed (query, key) pairs per (batch, head) of a doc-free causal frame mask (SURVEY §8(d)
-    counts algorithmic FLOPs over allowed pairs only).  Docs are ignored (upper bound)."""
+    """Allowed (query, key) pairs per (batch, head), averaged over the batch (SURVEY §8(d) counts
+    algorithmic FLOPs over allowed pairs only).  With document arrays the doc predicate is counted
+    exactly on the device (frame x frame; profiling only); without them the mask is doc-free."""
     tpf, w = mask.tpf, mask.window
     nfq = (Lq + tpf - 1) // tpf
     off = mask.q_offset // tpf
     tot = 0
+    if mask.arrays is not None and mask.causal:
+        doc = mask.arrays["doc"]
+        qf = torch.arange(off, off + nfq, device=doc.device)[:, None]
+        kf = torch.arange(doc.shape[1], device=doc.device)[None, :]
+        ok = kf <= qf
+        if w is not None:
+            ok &= kf > qf - w
+        same = doc[:, off:off + nfq, None] == doc[:, None, :]
+        return float((same & ok).sum().item()) / doc.shape[0] * tpf * tpf
     if not mask.causal:
         return float(Lq) * Lkv if w is None else float(Lq) * min(Lkv, (2 * w - 1) * tpf)
     for f in range(off, off + nfq):

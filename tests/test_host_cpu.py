@@ -254,3 +254,47 @@ def test_gemm_splitk_workspace_query():
     assert q(6144, 1536, 98304, 1, 1, 1, 0, 0, 0.0) == 0       # bf16 output
     assert q(98304, 6144, 98304, 1, 1, 1, 1, 0, 0.0) == 0      # enough tiles, no split
     assert q(6144, 1536, 98304, 1, 1, 1, 1, 0, 0.5) == 0       # beta other than 0 / 1
+
+
+@pytest.mark.parametrize("window", [None, 3])
+def test_mask_pairs_counts_documents(window):
+    """The algorithmic FLOP count (allowed pairs only) with document arrays equals a
+    brute-force count of the reference predicate (attn.py:24-62) and, for one document, the
+    analytic doc-free count."""
+    from owl_wms import kernels as K
+    tpf, nf = 4, 12
+    doc = torch.tensor([[0] * 5 + [1] * 4 + [2] * 3, [7] * 12])
+    m = K.FrameMask(tpf, window, arrays=K.frame_arrays(doc, nf, window))
+    brute = 0
+    for b in range(2):
+        for qf in range(nf):
+            for kf in range(nf):
+                ok = kf <= qf and (window is None or qf - kf < window) and bool(doc[b, qf] == doc[b, kf])
+                brute += ok * tpf * tpf
+    assert K.mask_pairs(m, nf * tpf, nf * tpf) == brute / 2
+    one = K.FrameMask(tpf, window, arrays=K.frame_arrays(doc[1:], nf, window))
+    assert K.mask_pairs(one, nf * tpf, nf * tpf) == K.mask_pairs(K.FrameMask(tpf, window), nf * tpf, nf * tpf)
+
+
+@pytest.mark.parametrize("window", [None, 1, 3])
+def test_frame_arrays_runs_form_is_exact(window):
+    """Packed (contiguous-run) documents: frame_arrays flags them and the range form the kernels
+    then use -- allowed(q, k) <=> kv_lo[q] <= k <= q <=> k <= q <= q_hi[k] -- equals the reference
+    predicate (attn.py:24-62) exactly; recurring documents are not flagged."""
+    from owl_wms.kernels import frame_arrays
+    g = torch.Generator().manual_seed(3)
+    nf = 23
+    for _ in range(6):
+        cuts = sorted(torch.randperm(nf - 1, generator=g)[:4].add(1).tolist())
+        doc = torch.zeros(1, nf, dtype=torch.long)
+        for i, c in enumerate(cuts):
+            doc[0, c:] = 10 * (i + 1)
+        a = frame_arrays(doc, nf, window)
+        assert a["runs"]
+        lo, hi = a["kv_lo"][0].tolist(), a["q_hi"][0].tolist()
+        for fq in range(nf):
+            for fk in range(nf):
+                ref = fk <= fq and (window is None or fq - fk < window) and bool(doc[0, fq] == doc[0, fk])
+                assert ref == (lo[fq] <= fk <= fq) == (fk <= fq <= hi[fk])
+    rec = torch.tensor([[0, 0, 1, 1, 0, 0]])
+    assert not frame_arrays(rec, 6, window)["runs"]

@@ -206,7 +206,19 @@ ATTN_CASES = [
     (2, 1, 9, 4, 3, True),
     (1, 2, 24, 64, 16, True),
     (1, 2, 7, 65, None, False),  # unwindowed, ragged inside the second 64-row half of a 128-row dK/dV tile
+    (2, 2, 8, 64, None, "split"),  # documents that recur (not one contiguous run): general doc path
+    (1, 2, 12, 64, 4, "split"),
 ]
+
+
+def _docs(B, nf, docs):
+    doc = torch.zeros(B, nf, dtype=torch.long)
+    if docs == "split":
+        doc[:] = (torch.arange(nf) // 2) % 2
+    elif docs:
+        doc[:, nf // 3:] = 1
+        doc[-1, 2 * nf // 3:] = 2
+    return doc
 
 
 @pytest.mark.parametrize("case,D", [(c, 64) for c in ATTN_CASES] + [(ATTN_CASES[i], 128) for i in (0, 2, 4, 6)])
@@ -216,11 +228,10 @@ def test_attention_fwd_bwd(case, D):
     B, H, nf, tpf, window, docs = case
     L = nf * tpf
     q, kk, v = rnd(B * L, H * D, seed=40), rnd(B * L, H * D, seed=41), rnd(B * L, H * D, seed=42)
-    doc = torch.zeros(B, nf, dtype=torch.long)
-    if docs:
-        doc[:, nf // 3:] = 1
-        doc[-1, 2 * nf // 3:] = 2
+    doc = _docs(B, nf, docs)
     arrays = k.frame_arrays(doc.to(DEV), nf, window) if docs else None
+    if docs:
+        assert arrays["runs"] == (docs is True)  # contiguous runs take the range form of the mask
     mask = k.FrameMask(tpf, window, True, 0, arrays)
     q, kk, v = (t.view(B, L, H * D) for t in (q, kk, v))
     o, lse = k.attn_fwd(q, kk, v, H, D, mask)
@@ -576,3 +587,36 @@ def test_gemm_skinny_splitk_epilogues(M, N, Kd):
     o = k.gemm(A, W, bias=bias, epi=k.EPI_GATE_RESID, gate=g, tpf=tpf, resid=res)
     gref = g.float().repeat_interleave(tpf, 0)[:M]
     assert rel(o, res.float() + gref * y) < 5e-3
+
+
+@pytest.mark.parametrize("case", [(2, 2, 12, 64, None), (1, 2, 24, 64, 16), (2, 1, 9, 4, 3), (1, 2, 7, 65, None),
+                                  (1, 2, 10, 64, 4)])
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_packed_runs_match_general_doc_path(case, D):
+    """Packed documents (contiguous runs, what the sequence-packing loader yields) through the
+    range form of the mask (kv_lo / q_hi only) give the same O, lse, dQ, dK, dV as the general
+    per-element document path, and match the oracle."""
+    k = K()
+    B, H, nf, tpf, window = case
+    L = nf * tpf
+    doc = torch.zeros(B, nf, dtype=torch.long)
+    doc[0, 3:] = 1
+    doc[0, nf - 2:] = 2
+    if B > 1:
+        doc[1, nf // 2:] = 7
+    arrays = k.frame_arrays(doc.to(DEV), nf, window)
+    assert arrays["runs"]
+    q, kk, v = (rnd(B * L, H * D, seed=s).view(B, L, H * D) for s in (90, 91, 92))
+    do = rnd(B * L, H * D, seed=93).view(B, L, H * D)
+    res = []
+    for runs in (True, False):
+        mask = k.FrameMask(tpf, window, True, 0, dict(arrays, runs=runs))
+        o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+        dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+        k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, dq, dk, dv)
+        res.append((o, lse, dq, dk, dv))
+    for a, b in zip(*res):
+        assert rel(a, b) < 1e-5
+    ref = R.attention(*(t.cpu().float().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v)),
+                      R.frame_mask(L, L, tpf, window, doc))
+    assert rel(res[0][0].view(B, L, H, D).transpose(1, 2), ref) < 1e-2
