@@ -918,6 +918,9 @@ __global__ __launch_bounds__(256) void splitk_epi_k(GemmP p, int splits) {
         v[e + 4] = hi[e];
       }
     }
+    // unrolled so the loads of several splits are in flight at once (the reduce is latency-bound
+    // at decode sizes: M = 1..64 rows, a few hundred threads); the adds stay in split order
+#pragma unroll 8
     for (int sp = 1; sp < splits; ++sp) {
       const f32x4 lo = __builtin_nontemporal_load((const f32x4*)(w + sp * MN));
       const f32x4 hi = __builtin_nontemporal_load((const f32x4*)(w + sp * MN + 4));
