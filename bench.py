@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="override n_frames (default: the config's)")
     ap.add_argument("--docs", type=int, default=1,
                     help="documents per packed sample (SURVEY §8(d) doc-mask variant: 4 x 384 frames)")
+    ap.add_argument("--ckpt-layers", type=int, default=None,
+                    help="checkpoint only the first N blocks (configs with gradient_checkpointing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--config", default="configs/dit_v4.yml",
@@ -121,6 +123,8 @@ def main():
     cfg_name = os.path.splitext(os.path.basename(args.config))[0]
     headline = cfg_name == "dit_v4" and args.docs == 1
     mc = cfg.model
+    if args.ckpt_layers is not None:
+        mc.checkpoint_layers = args.ckpt_layers
     if args.frames:
         mc.n_frames = args.frames
     tokens = mc.n_frames * mc.tokens_per_frame  # joint video + audio tokens for game_rft_audio
@@ -230,6 +234,7 @@ def main():
             for k, (n, ms_, fl_) in kernels[:40]:
                 log(f"  {k:60s} n={n:3d} {ms_:9.3f} ms  {fl_ / max(ms_, 1e-9) / 1e9:8.1f} TF/s")
             log(f"  total kernel time {tot_ms:.1f} ms")
+        log(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:

@@ -194,10 +194,14 @@ class DiT(nn.Module):
             global_block_mask = self.get_block_mask(seq_len, doc_id, getattr(self.config, "global_window", None),
                                                     q_offset, device)
         ckpt = self.training and getattr(self.config, "gradient_checkpointing", False) and kv_cache is None
+        # optional: checkpoint only the first `checkpoint_layers` blocks and keep the rest's activations
+        # (HBM headroom on a 288 GB MI355X trades for the recompute); default = every block, as the reference
+        n_ck = getattr(self.config, "checkpoint_layers", None)
         for i, block in enumerate(self.blocks):
             mask = local_block_mask if self.local_layers[i] else global_block_mask
-            block._checkpointed = ckpt  # the re-run inside backward reuses the kept attention output
-            x = checkpoint(block, x, cond, mask, kv_cache) if ckpt else block(x, cond, mask, kv_cache)
+            ck = ckpt and (n_ck is None or i < n_ck)
+            block._checkpointed = ck  # the re-run inside backward reuses the kept attention output
+            x = checkpoint(block, x, cond, mask, kv_cache) if ck else block(x, cond, mask, kv_cache)
         return x
 
 

@@ -278,8 +278,11 @@ def test_checkpointed_blocks_reuse_attention():
     from owl_wms.models.gamerft import GameRFT
     p = "gamerft.bf16."
     grads, losses, nfwd = [], [], []
-    for ckpt in (False, True):
-        m = det_init_(GameRFT(model_config(**TINY, gradient_checkpointing=ckpt)), base_seed=1000).cuda().train()
+    for ckpt, n_ck in ((False, None), (True, None), (True, 1)):  # n_ck: checkpoint_layers (first n only)
+        kw = dict(TINY, gradient_checkpointing=ckpt)
+        if n_ck is not None:
+            kw["checkpoint_layers"] = n_ck
+        m = det_init_(GameRFT(model_config(**kw)), base_seed=1000).cuda().train()
         m.noise_source = InjectedNoise({"rand_b": GR[p + "in.rand_b"], "ts_raw": GR[p + "in.ts_raw"],
                                         "z": GR[p + "in.z"]})
         _lib.profile_begin()
@@ -290,11 +293,12 @@ def test_checkpointed_blocks_reuse_attention():
         nfwd.append(sum(n for k, (n, _, _) in prof.items() if k.startswith("attn_fwd")))
         losses.append(loss.item())
         grads.append({k: q.grad.detach().clone() for k, q in m.named_parameters() if q.grad is not None})
-    assert nfwd == [TINY["n_layers"], TINY["n_layers"]]
-    assert losses[0] == losses[1]
-    assert grads[0].keys() == grads[1].keys()
-    for k in grads[0]:
-        assert rel(grads[1][k], grads[0][k]) < 1e-6, k
+    assert nfwd == [TINY["n_layers"]] * 3
+    for j in (1, 2):
+        assert losses[0] == losses[j]
+        assert grads[0].keys() == grads[j].keys()
+        for k in grads[0]:
+            assert rel(grads[j][k], grads[0][k]) < 1e-6, k
 
 
 def _packed_table(path, lens, seed=0):
