@@ -99,11 +99,14 @@ class Attn(nn.Module):
         k = qkr.view(B, L, 2 * d)[:, :, d:]
         v = qkv.view(B, L, 3 * d)[:, :, 2 * d:]
         if offset > 0:
-            old_k, old_v = kv_cache.get(self.layer_idx)
-            k = torch.cat([old_k, k], dim=1)
-            v = torch.cat([old_v, v], dim=1)
+            if kv_cache.noise_caches == 0.0 and hasattr(kv_cache, "extend"):
+                k, v = kv_cache.extend(self.layer_idx, k, v)  # [cache | new] in place, no torch.cat
+            else:
+                old_k, old_v = kv_cache.get(self.layer_idx)
+                k = torch.cat([old_k, k], dim=1)
+                v = torch.cat([old_v, v], dim=1)
         if kv_cache is not None and kv_cache.should_update:
-            kv_cache.update(k.contiguous(), v.contiguous(), self.layer_idx)
+            kv_cache.update(k, v, self.layer_idx)
         if block_mask is None:  # decoding: unmasked over [cache | new] (attn.py:101-107)
             if self.local:
                 k, v = k[:, -self.local_offset:], v[:, -self.local_offset:]

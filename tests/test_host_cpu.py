@@ -298,3 +298,43 @@ def test_frame_arrays_runs_form_is_exact(window):
                 assert ref == (lo[fq] <= fk <= fq) == (fk <= fq <= hi[fk])
     rec = torch.tensor([[0, 0, 1, 1, 0, 0]])
     assert not frame_arrays(rec, 6, window)["runs"]
+
+
+def test_kv_cache_extend_matches_cat_model():
+    """The preallocated KV cache (kv_cache.py:5-104 API): extend == torch.cat([cache, new]) with the
+    cache unchanged until update commits it; update / truncate (both ends) / get / offsets behave as
+    the reference's list-of-tensors cache, across buffer growth and compaction."""
+    from types import SimpleNamespace
+    from owl_wms.nn.kv_cache import SingleKVCache
+    cfg = SimpleNamespace(n_layers=2, tokens_per_frame=4)
+    c = SingleKVCache(cfg)
+    c.reset(2)
+    g = torch.Generator().manual_seed(0)
+    new = lambda n: torch.randn(2, n, 8, generator=g)
+    ref = []
+    for i in range(2):
+        k, v = new(12), new(12)
+        c.update(k[:, :], v, i)
+        ref.append((k.clone(), v.clone()))
+    off = [12, 12]
+    for step in range(30):
+        for i in range(2):
+            kn, vn = new(4), new(4)
+            K_, V_ = c.extend(i, kn, vn)
+            RK, RV = torch.cat([ref[i][0], kn], 1), torch.cat([ref[i][1], vn], 1)
+            assert torch.equal(K_, RK) and torch.equal(V_, RV)
+            if step % 3 == 0:
+                c.update(K_, V_, i)
+                ref[i] = (RK, RV)
+                off[i] += 4
+        if step % 7 == 6:
+            c.truncate(1, front=False)
+            ref = [(a[:, 4:], b[:, 4:]) for a, b in ref]
+        if step % 11 == 10:
+            c.truncate(1, front=True)
+            ref = [(a[:, :-4], b[:, :-4]) for a, b in ref]
+        for i in range(2):
+            k, v = c.get(i)
+            assert torch.equal(k, ref[i][0]) and torch.equal(v, ref[i][1])
+            assert c.length_at(i) == ref[i][0].shape[1]
+    assert c.offsets == off
