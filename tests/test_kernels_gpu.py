@@ -620,3 +620,30 @@ def test_attention_packed_runs_match_general_doc_path(case, D):
     ref = R.attention(*(t.cpu().float().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v)),
                       R.frame_mask(L, L, tpf, window, doc))
     assert rel(res[0][0].view(B, L, H, D).transpose(1, 2), ref) < 1e-2
+
+
+def test_muon_multirank_path_on_gpu(monkeypatch):
+    """The world_size > 1 branch of Muon.step (round-robin NS + all_gather, muon.py:86-115) on the
+    HIP passes, in one process: the gather is emulated so that this rank's update lands in its slot,
+    and the parameters this rank owns must equal a single-rank step of the same parameters."""
+    import owl_wms.muon as mu
+    gen = torch.Generator().manual_seed(31)
+    shapes = [(96, 64), (96, 64), (96, 64)]
+    p0 = [torch.randn(s, generator=gen).to(DEV) for s in shapes]
+    gs = [torch.randn(s, generator=gen).to(DEV) for s in shapes]
+
+    def run(ws, rank):
+        ps = [torch.nn.Parameter(p.clone()) for p in p0]
+        for p, g in zip(ps, gs):
+            p.grad = g.clone()
+        mu.Muon(ps, lr=1e-2, momentum=0.95, rank=rank, world_size=ws).step()
+        return ps
+
+    def fake_gather(out, inp):  # slot `rank` gets this rank's update, the other slot a copy of it
+        out.copy_(inp.expand_as(out))
+
+    monkeypatch.setattr(mu, "_all_gather", fake_gather)
+    single = run(1, 0)
+    multi = run(2, 0)  # rank 0 of 2 owns params 0 and 2 (chunks [0, 1], [2])
+    for i in (0, 2):
+        assert rel(multi[i].detach() - p0[i], single[i].detach() - p0[i]) < 1e-2
