@@ -387,3 +387,54 @@ def test_graphed_decode_equals_eager(n_steps, cfg):
         outs.append(s(m.core, x, mouse, btn, compile_on_decode=graphed))
     assert outs[0].shape == (2, 8, 32, 8, 8)
     assert torch.equal(outs[0], outs[1])
+
+
+def _dp_worker(rank, ws, port, q):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=ws)  # gloo on GPU tensors: one card, 2 ranks
+    try:
+        from owl_wms.muon import init_muon
+        from owl_wms.utils.grad_reducer import GradReducer
+        torch.cuda.set_device(0)
+        m = _model()
+        kw = dict(lr=1e-3, momentum=0.95, adamw_lr=1e-4, adamw_wd=1e-4, adamw_eps=1e-15, adamw_betas=[0.9, 0.95],
+                  adamw_keys=["core.proj_in", "core.proj_out.proj", "core.t_embed", "core.control_embed", "gate",
+                              "adaln"])
+        opt = init_muon(m, rank=rank, world_size=ws, **kw)
+        red = GradReducer(m.parameters(), world_size=ws)
+        g = torch.Generator().manual_seed(100 + rank)
+        for micro in range(2):
+            red.begin(sync=micro == 1)
+            x = torch.randn(1, 8, 32, 8, 8, generator=g).bfloat16().cuda()
+            mouse = torch.randn(1, 8, 2, generator=g).bfloat16().cuda()
+            btn = (torch.rand(1, 8, 11, generator=g) < 0.5).bfloat16().cuda()
+            (m(x, mouse, btn, torch.zeros(1, 8, dtype=torch.long).cuda()) / 2).backward()
+            red.finish()
+        opt.step()
+        torch.cuda.synchronize()
+        q.put((rank, {k: p.detach().cpu().numpy() for k, p in m.named_parameters()}))  # plain bytes
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_step_two_ranks_on_gpu():
+    """The N > 1 training step on GPU tensors (2 ranks sharing the card over gloo; RCCL needs one
+    GPU per rank): bucketed grad all-reduce, distributed Muon (round-robin NS + all_gather) and
+    AdamW on the HIP passes -- replicas must be bit-identical afterwards."""
+    import os as _os
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + _os.getpid() % 1000
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    assert res[0].keys() == res[1].keys()
+    for k in res[0]:
+        assert (res[0][k] == res[1][k]).all(), k
