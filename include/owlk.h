@@ -154,6 +154,9 @@ int owlk_muon_apply(int count, float* const* p, const void* u, long rows, long c
 int owlk_adamw(int count, float* const* p, const float* const* g, float* const* m, float* const* v, const long* n,
                float lr, float beta1, float beta2, float weight_decay, float eps, float step_size, float bc2_sqrt,
                void* stream);
+/* EMA of the weights (rft_trainer.py:105, ema_pytorch): shadow[i] = lerp(shadow[i], p[i], weight) over
+ * `count` fp32 tensors of n[i] elements, torch's lerp formula (weight = 1 - decay). */
+int owlk_ema(int count, float* const* shadow, const float* const* p, const long* n, float weight, void* stream);
 
 /* ---- MMDiT plumbing (frames.hip) ----
  * owlk_frame_mux replaces the per-frame concat / split of mmattn.py:54-60 and :77-80: frame f of

@@ -168,6 +168,34 @@ __global__ __launch_bounds__(256) void adamw_k(AdamPtrs A, float decay, float b1
   }
 }
 
+
+// EMA of the weights (ema_pytorch as restated in utils/grad_reducer.py): shadow = lerp(shadow, p, w),
+// torch's lerp formula, over up to kMaxA tensors of any sizes per launch.
+struct LerpPtrs {
+  float* s[kMaxA];
+  const float* p[kMaxA];
+  long n[kMaxA];
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void ema_k(LerpPtrs E, float w) {
+  const int z = blockIdx.y;
+  float* __restrict__ sh = E.s[z];
+  const float* __restrict__ p = E.p[z];
+  const long n = E.n[z];
+  if (VEC) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < (n >> 2); i += (long)gridDim.x * 256) {
+      f32x4 a = reinterpret_cast<const f32x4*>(sh)[i];
+      const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = lerp_t(a[j], b[j], w);
+      reinterpret_cast<f32x4*>(sh)[i] = a;
+    }
+  } else {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) sh[i] = lerp_t(sh[i], p[i], w);
+  }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 unsigned flat_blocks(long work, int count) {
@@ -257,4 +285,31 @@ extern "C" int owlk_adamw(int count, float* const* p, const float* const* g, flo
       hipLaunchKernelGGL(adamw_k<false>, grid, dim3(256), 0, s, A, decay, beta1, beta2, step_size, bc2_sqrt, eps);
   }
   return owlk::check_launch("adamw");
+}
+
+extern "C" int owlk_ema(int count, float* const* shadow, const float* const* p, const long* n, float weight,
+                        void* stream) {
+  OWLK_REQUIRE(count >= 0 && shadow && p && n, "ema: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  for (int base = 0; base < count; base += kMaxA) {
+    const int k = count - base < kMaxA ? count - base : kMaxA;
+    LerpPtrs E{};
+    bool vec = true;
+    long nmax = 1;
+    for (int i = 0; i < k; ++i) {
+      const int j = base + i;
+      OWLK_REQUIRE(shadow[j] && p[j] && n[j] > 0, "ema: null tensor or empty size");
+      E.s[i] = shadow[j];
+      E.p[i] = p[j];
+      E.n[i] = n[j];
+      vec = vec && (n[j] % 4) == 0 && aligned16(shadow[j]) && aligned16(p[j]);
+      nmax = n[j] > nmax ? n[j] : nmax;
+    }
+    const dim3 grid(flat_blocks(vec ? nmax / 4 : nmax, k), (unsigned)k);
+    if (vec)
+      hipLaunchKernelGGL(ema_k<true>, grid, dim3(256), 0, s, E, weight);
+    else
+      hipLaunchKernelGGL(ema_k<false>, grid, dim3(256), 0, s, E, weight);
+  }
+  return owlk::check_launch("ema");
 }

@@ -43,6 +43,7 @@ _SIGS = {
     "owlk_muon_momentum": [I, P, P, L, F, I, P, P, P],
     "owlk_muon_apply": [I, P, P, L, L, I, F, F, P],
     "owlk_adamw": [I, P, P, P, P, P, F, F, F, F, F, F, F, P],
+    "owlk_ema": [I, P, P, P, F, P],
 }
 
 _RESTYPES = {"owlk_gemm_splitk_bytes": ctypes.c_long}  # size queries; every other entry returns an int status

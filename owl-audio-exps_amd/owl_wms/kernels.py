@@ -375,6 +375,18 @@ def adamw(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, weight_decay, 
          float(weight_decay), float(eps), float(step_size), float(bc2s), stream())
 
 
+def ema_lerp(shadow, params, weight):
+    """shadow[i] = lerp(shadow[i], params[i], weight) in one multi-tensor pass (owlk_ema)."""
+    import ctypes
+    assert len(shadow) == len(params)
+    for a, b in zip(shadow, params):
+        assert a.dtype == F32 and b.dtype == F32 and a.is_contiguous() and b.is_contiguous() and a.is_cuda
+        assert a.numel() == b.numel()
+    ns = [t.numel() for t in shadow]
+    call("owlk_ema", len(shadow), _ptr_array(shadow), _ptr_array(params), (ctypes.c_long * len(ns))(*ns),
+         float(weight), stream())
+
+
 # ---------------------------------------------------------------- MMDiT plumbing (frames.hip)
 def frame_interleave(a, b, n0, n1, out=None):
     """a [F*n0, C], b [F*n1, C] token-major -> joint [F*(n0+n1), C] (frame f = a-rows | b-rows)."""

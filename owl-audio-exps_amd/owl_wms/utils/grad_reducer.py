@@ -118,7 +118,8 @@ class EMA:
             return
         epoch = max(step - self.after - 1, 0)
         decay = 0.0 if epoch <= 0 else min(self.beta, 1 - (1 + epoch / self.inv_gamma) ** -self.power)
-        torch._foreach_lerp_(self.shadow, [p.detach() for p in self.params], 1.0 - decay)
+        from .. import kernels as K
+        K.ema_lerp(self.shadow, [p.detach() for p in self.params], 1.0 - decay)  # one libowlk pass (owlk_ema)
 
     def state_dict(self):
         names = [n for n, _ in self.model.named_parameters()]
