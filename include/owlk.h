@@ -28,15 +28,17 @@ int owlk_device_ok(void);
  *       2 GATE_RESID aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m / tpf, n] * y))
  *       3 DSILU      C = bf16(bf16(acc) * silu'(aux))
  *       4 AXPBY      C = bf16(bf16(alpha * bf16(acc)) + bf16(beta * aux))
+ *       5 SCALE2     C = bf16(acc); aux = bf16(alpha * bf16(acc))   (a_trans = b_trans = 0 only)
  *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes.
  *   fp32 STORE with beta 0 or 1 and K >= 8192 onto a small output (weight gradients) splits K
- *   over workgroups.  With a caller-owned workspace of owlk_gemm_splitk_bytes(...) bytes (ws,
- *   16-B aligned) the per-split partials go there and one fixed-order reduce forms C: the result
- *   is deterministic.  Without it (ws null or too small) the splits combine by fp32 atomics onto
- *   C (cleared first when beta = 0).  The library never allocates.
+ *   over workgroups.  With a caller-owned workspace of owlk_gemm_ws_bytes(...) bytes (ws, 16-B
+ *   aligned) the per-split partials go there and one fixed-order reduce forms C: the result is
+ *   bitwise deterministic.  Without it (ws null or too small) the splits combine by fp32 atomics
+ *   onto C (cleared first when beta = 0).  The library never allocates.
  *   colsum (optional, batch 1, bf16 C): colsum[n] += sum_m C[m, n] over the stored bf16 values
  *   (bias gradient of the next layer, fused into the DSILU epilogue of the 256^2 kernel; a
- *   separate column-sum pass otherwise).  Caller zeroes it. */
+ *   separate column-sum pass otherwise); deterministic with the workspace (per-tile partial rows
+ *   added in order), fp32 atomics without.  It accumulates onto colsum. */
 int owlk_gemm(long M, long N, long K, long batch,
               const void* A, long lda, long sA, int a_trans,
               const void* B, long ldb, long sB, int b_trans,
@@ -49,6 +51,10 @@ int owlk_gemm(long M, long N, long K, long batch,
 /* bytes of split-K workspace owlk_gemm uses for these arguments (0: no split) */
 long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta);
+/* bytes of workspace for the deterministic form of a call: split-K partials, and with colsum != 0
+ * the column-sum partials (fused or separate pass) */
+long owlk_gemm_ws_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
+                        float beta, int colsum);
 
 /* ---- AdaLN modulate (modulation.py:7-26 AdaLN.forward after its fc; :46-55 cond_adaln):
  *   y[t] = bf16(bf16(bf16(rms_norm(x[t])) * bf16(1 + scale[t/tpf])) + shift[t/tpf]); rstd[t] fp32 */
@@ -124,22 +130,46 @@ int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out, void* str
 /* MSE (gamerft.py:111): partial[block] = sum (pred - tgt)^2; dpred = bf16(gscale * (pred - tgt)) */
 int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,
              int nblocks, void* stream);
-/* out[n] += sum_r x[r, n] (bias gradients); x bf16 (x_f32 = 0) or fp32 */
-int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream);
+/* out[n] += sum_r x[r, n] (bias gradients); x bf16 (x_f32 = 0) or fp32.  With ws (>=
+ * owlk_colsum_ws_bytes(R, N) bytes, 16-B aligned) row splits store partial rows that one pass adds
+ * in order (bitwise deterministic); without it the splits combine by fp32 atomics. */
+long owlk_colsum_ws_bytes(long R, long N);
+int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* ws, long ws_bytes,
+                void* stream);
 
-/* ---- Newton-Schulz (muon.py:11-38) helpers: X /= (||X||_F + eps) per batch item, bf16 */
+/* ---- Newton-Schulz (muon.py:11-38) helpers: X /= (||X||_F + eps) per batch item, bf16.
+ * Norms are reduced without atomics: sum-of-squares passes write OWLK_NORM_PARTS partial sums per
+ * matrix and the scale pass adds them in fixed order (bitwise reproducible).
+ * work: fp32 [batch, OWLK_NORM_PARTS] scratch (fully written; no zeroing needed). */
+#define OWLK_NORM_PARTS 256
 int owlk_ns_normalize(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
                       float* work, void* stream);
-/* the scale pass of owlk_ns_normalize alone, given sumsq[batch] = sum(bf16(g)^2) per matrix */
+/* the scale pass of owlk_ns_normalize alone, given sumsq [batch, OWLK_NORM_PARTS] partials of
+ * sum(bf16(g)^2) per matrix (what owlk_muon_momentum writes) */
 int owlk_ns_scale(const void* g, int g_f32, long rows, long cols, long batch, int transpose, void* x,
                   const float* sumsq, void* stream);
+/* The quintic iterations of muon.py:30-34, in place on a normalised bf16 X [batch, m, k]
+ *   (contiguous, m <= k, both multiples of 8), in the eager reference's rounding order:
+ *   A = X X^T; B = bf16(b A) + bf16(bf16(c A) @ A); X = bf16(a X) + bf16(B @ X).
+ *   ws: caller-owned, >= owlk_ns_iterate_ws_bytes(batch, m, k) bytes, 16-B aligned. */
+long owlk_ns_iterate_ws_bytes(long batch, long m, long k);
+int owlk_ns_iterate(void* x, long batch, long m, long k, int steps, float a, float b, float c, void* ws,
+                    long ws_bytes, void* stream);
+/* zeropower_via_newtonschulz5 (muon.py:11-38) as one entry: g [batch, rows, cols] fp32 (g_f32 = 1)
+ *   or bf16 -> out bf16 [batch, rows, cols]; transposes when rows > cols and zero-pads dims that
+ *   are not multiples of 8 internally.  Reference coefficients (a, b, c) = (3.4445, -4.7750, 2.0315).
+ *   ws: caller-owned, >= owlk_newton_schulz_ws_bytes(batch, rows, cols) bytes, 16-B aligned. */
+long owlk_newton_schulz_ws_bytes(long batch, long rows, long cols);
+int owlk_newton_schulz_bf16(const void* g, int g_f32, long batch, long rows, long cols, int steps, float a,
+                            float b, float c, void* out, void* ws, long ws_bytes, void* stream);
 
 /* ---- fused Muon passes (optim.hip; replace muon.py:66-84's torch elementwise ops) ----
  * owlk_muon_momentum: for each of `count` fp32 matrices of n elements (host array of device
  *   pointers g[i], buf[i]): buf = lerp(buf, g, 1 - momentum); g' = nesterov ? lerp(g, buf, momentum)
  *   : buf (muon.py:67-73).  g' goes to stack[i*n ...] (fp32, the batched NS input) or, with
- *   stack == NULL, back into g (the reference's in-place update).  sumsq[i] += sum(bf16(g')^2)
- *   (caller zeroes it; NULL skips), the Frobenius-norm input of owlk_ns_scale (muon.py:24-26).
+ *   stack == NULL, back into g (the reference's in-place update).  sumsq: fp32 [count,
+ *   OWLK_NORM_PARTS], written with the partial sums of sum(bf16(g')^2) (NULL skips), the
+ *   Frobenius-norm input of owlk_ns_scale (muon.py:24-26).
  * owlk_muon_apply: p[i] = p[i] * decay - alpha * u[i] (muon.py:80-84: decay = 1 - lr*wd,
  *   alpha = lr * max(1, rows/cols)^0.5); u bf16 [count, rows, cols], or [count, cols, rows] with
  *   transpose = 1 (the NS iterate before its transpose back). */

@@ -179,14 +179,11 @@ def sincos(x, dim, theta=300.0, mult=1000.0):
 NS_COEF = (3.4445, -4.7750, 2.0315)
 
 
-def newton_schulz5(G, steps=5, order="eager"):
-    """muon.py:11-38: quintic Newton-Schulz in bf16.
-
-    order="eager": the reference's eager rounding, B = bf16(b*A) + bf16(bf16(c*A) @ A).
-    order="epilogue": the same math with the scalar applied after the product,
-    B = bf16(b*A) + bf16(c * bf16(A @ A^T)), as libowlk's AXPBY GEMM epilogue rounds it.
-    (bf16 NS is chaotic in its rounding order: the two orders differ by ~2.7% rel-L2.)
-    """
+def newton_schulz5(G, steps=5):
+    """muon.py:11-38: quintic Newton-Schulz in bf16, in the eager reference's rounding order:
+    A = X X^T; B = bf16(b*A) + bf16(bf16(c*A) @ A) (`c * A @ A` is `(c*A) @ A`); X = bf16(a*X) +
+    bf16(B @ X).  (bf16 NS is chaotic in its rounding order: another valid order, e.g. c applied
+    after the product, differs by ~2.7% rel-L2 after 5 steps.)"""
     a, b, c = NS_COEF
     X = G.bfloat16()
     tr = G.size(-2) > G.size(-1)
@@ -195,7 +192,7 @@ def newton_schulz5(G, steps=5, order="eager"):
     X = X / (X.norm(dim=(-2, -1), keepdim=True) + 1e-7)
     for _ in range(steps):
         A = X @ X.mT
-        B = b * A + c * A @ A if order == "eager" else b * A + c * (A @ A.mT)
+        B = b * A + c * A @ A
         X = a * X + B @ X
     if tr:
         X = X.mT

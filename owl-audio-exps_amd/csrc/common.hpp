@@ -55,6 +55,21 @@ DEV float wave_sum(float v) {
   return v;
 }
 
+// Frobenius-norm partials: the sum-of-squares passes write kNormParts per-block partial sums per
+// matrix (no atomics) and the consumer adds them in index order, so the norm is bitwise
+// reproducible (OWLK_NORM_PARTS in include/owlk.h).
+constexpr int kNormParts = 256;
+
+// fixed-order sum of a 256-thread block's values (wave butterflies, then the 4 wave sums in order)
+DEV float block_sum256(float v, float* red4) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = ((red4[0] + red4[1]) + red4[2]) + red4[3];
+  __syncthreads();
+  return r;
+}
+
 DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -80,6 +95,8 @@ DEV bf16x8 pack8(const float* f) {
 namespace owlk {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// out[n] += sum_s part[s][n], s = 0 .. splits-1 in order (fp32, N % 4 == 0, 16-B aligned)
+int colsum_reduce(const float* part, int splits, long N, float* out, hipStream_t s);
 }  // namespace owlk
 #define OWLK_REQUIRE(cond, ...)             \
   do {                                      \

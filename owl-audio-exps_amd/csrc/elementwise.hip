@@ -377,10 +377,12 @@ __global__ __launch_bounds__(256) void mse_k(const bf16* __restrict__ pred, cons
 }
 
 // ------------------------------------------------------------------ column sums (bias grads)
-// out[n] (+)= sum_r x[r, n]; x bf16 or fp32; grid.y splits the rows, fp32 atomics combine
+// out[n] (+)= sum_r x[r, n]; x bf16 or fp32; grid.y splits the rows.  With a workspace each split
+// stores its partial row (part[split][n]) and colsum_reduce_k adds them onto out in split order
+// (bitwise reproducible); without one, fp32 atomics combine the splits.
 template <typename T, int U>
 __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R, long N, long ld, long rows_per,
-                                                float* __restrict__ out) {
+                                                float* __restrict__ out, float* __restrict__ part) {
   const long col = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
   if (col >= N) return;
   const long r0 = (long)blockIdx.y * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
@@ -407,8 +409,31 @@ __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R,
     for (int u = 0; u < U; ++u) add_row(r + u);
   }
   for (; r < r1; ++r) add_row(r);
+  if (part) {
+    float* dst = part + (long)blockIdx.y * N + col;
+    *(f32x4*)dst = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    *(f32x4*)(dst + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) atomicAdd(out + col + e, acc[e]);
+}
+
+// out[n] += sum_s part[s][n] in split order (N % 4 == 0); shared with the GEMM's fused column sums
+__global__ __launch_bounds__(256) void colsum_reduce_k(const float* __restrict__ part, int splits, long N,
+                                                            float* __restrict__ out) {
+  const long n = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (n >= N) return;
+  f32x4 a = *(const f32x4*)(part + n);
+  for (int sp = 1; sp < splits; ++sp) {
+    const f32x4 b = *(const f32x4*)(part + (long)sp * N + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] += b[e];
+  }
+  f32x4 o = *(f32x4*)(out + n);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] += a[e];
+  *(f32x4*)(out + n) = o;
 }
 
 // ------------------------------------------------------------------ attention-bwd preprocess
@@ -526,25 +551,47 @@ extern "C" int owlk_mse(const void* pred, const void* tgt, long n, float gscale,
   return owlk::check_launch("mse");
 }
 
-extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream) {
-  OWLK_REQUIRE(N % 8 == 0 && ld % 8 == 0, "colsum: N, ld must be multiples of 8");
+// enough row splits to fill the chip (~2k workgroups), but >= 16 rows per workgroup: in the atomic
+// form every split adds N atomics onto the same N outputs, and short splits turn into same-address
+// contention (<= 512 adders per output: 2048 splits onto N = 1536 ran at 0.66 TB/s)
+static long colsum_splits(long R, long N, long* rows_per) {
   const long cols_blocks = (N / 8 + 255) / 256;
-  // enough row splits to fill the chip (~2k workgroups), but >= 16 rows per workgroup: every split
-  // adds N atomics onto the same N outputs, and short splits turn into same-address contention
-  // (<= 512 adders per output: 2048 splits onto N = 1536 ran at 0.66 TB/s, contention-bound)
   long splits = 2048 / cols_blocks;
   if (splits > 512) splits = 512;
   if (splits > R / 16) splits = R / 16;
   if (splits < 1) splits = 1;
-  const long rows_per = (R + splits - 1) / splits;
-  dim3 g((unsigned)cols_blocks, (unsigned)((R + rows_per - 1) / rows_per));
+  const long rp = (R + splits - 1) / splits;
+  if (rows_per) *rows_per = rp;
+  return (R + rp - 1) / rp;
+}
+
+extern "C" long owlk_colsum_ws_bytes(long R, long N) {
+  if (R <= 0 || N <= 0) return 0;
+  return colsum_splits(R, N, nullptr) * N * (long)sizeof(float);
+}
+
+extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* ws, long ws_bytes,
+                           void* stream) {
+  OWLK_REQUIRE(N % 8 == 0 && ld % 8 == 0, "colsum: N, ld must be multiples of 8");
+  OWLK_REQUIRE(((uintptr_t)out & 15) == 0, "colsum: out must be 16-byte aligned");
+  long rows_per;
+  const long splits = colsum_splits(R, N, &rows_per);
+  const long cols_blocks = (N / 8 + 255) / 256;
+  float* part = (ws && ws_bytes >= splits * N * (long)sizeof(float) && ((uintptr_t)ws & 15) == 0) ? (float*)ws
+                                                                                                   : nullptr;
+  dim3 g((unsigned)cols_blocks, (unsigned)splits);
+  hipStream_t s = (hipStream_t)stream;
   if (x_f32)
-    hipLaunchKernelGGL((colsum_k<float, 4>), g, dim3(256), 0, (hipStream_t)stream, (const float*)x, R, N, ld,
-                       rows_per, out);
+    hipLaunchKernelGGL((colsum_k<float, 4>), g, dim3(256), 0, s, (const float*)x, R, N, ld, rows_per, out, part);
   else
-    hipLaunchKernelGGL((colsum_k<bf16, 8>), g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, R, N, ld, rows_per,
-                       out);
+    hipLaunchKernelGGL((colsum_k<bf16, 8>), g, dim3(256), 0, s, (const bf16*)x, R, N, ld, rows_per, out, part);
+  if (part) return owlk::colsum_reduce(part, (int)splits, N, out, s);
   return owlk::check_launch("colsum");
+}
+
+int owlk::colsum_reduce(const float* part, int splits, long N, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_reduce_k, dim3((unsigned)((N / 4 + 255) / 256)), dim3(256), 0, s, part, splits, N, out);
+  return owlk::check_launch("colsum_reduce");
 }
 
 extern "C" int owlk_attn_delta(const void* o, const void* dout, long ld, long B, long L, int H, int D, float* delta,

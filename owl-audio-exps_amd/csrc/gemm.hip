@@ -25,6 +25,7 @@ enum Epi : int {
   EPI_GATE_RESID = 2,  // aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m/tpf]*y))
   EPI_DSILU = 3,       // C = bf16(bf16(acc) * silu'(aux))                        (MLP fc1 bwd)
   EPI_AXPBY = 4,       // C = bf16(bf16(alpha*bf16(acc)) + bf16(beta*aux))        (Newton-Schulz)
+  EPI_SCALE2 = 5,      // C = bf16(acc); aux = bf16(alpha*bf16(acc))   (NS: A = X X^T and c*A, muon.py:32-33)
 };
 
 constexpr int BK = 64;
@@ -45,6 +46,7 @@ struct GemmP {
   float* ws;    // split-K partials [split][M][N] (256^2 kernel); null: fp32 atomics combine the splits
   float* colsum_req;  // caller wants colsum[n] += sum_m C[m, n] (stored bf16 values)
   float* colsum;      // ... and the launched kernel fuses it (set by the dispatch, else a separate pass)
+  float* cs_part;     // fused column sums as per-(tile row, wave row) partials [tiles_m * 2][N] (deterministic)
 };
 
 // 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
@@ -200,6 +202,15 @@ DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * x[e]));
     *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+  } else if (EPI == EPI_SCALE2) {
+    float y[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      y[e] = rb(v[e]);
+      o[e] = rb(p.alpha * y[e]);
+    }
+    *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(y);
+    *(bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn) = pack8(o);
   }
 }
 
@@ -274,6 +285,15 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = rb(rb(p.alpha * rb(v[e])) + rb(p.beta * xx[e]));
     st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
+  } else if (EPI == EPI_SCALE2) {
+    float y[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      y[e] = rb(v[e]);
+      o[e] = rb(p.alpha * y[e]);
+    }
+    st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(y));
+    st_nt((bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), pack8(o));
   }
 }
 
@@ -797,8 +817,14 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
       cs[e] += __shfl_xor(cs[e], 32, 64);
     }
     if (lane < 8) {
+      if (p.cs_part) {  // this wave's partial row; colsum_reduce adds the rows in order afterwards
+        float* dst = p.cs_part + (long)(2 * tm + wr) * p.N + gn;
+        *(f32x4*)dst = f32x4{cs[0], cs[1], cs[2], cs[3]};
+        *(f32x4*)(dst + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(p.colsum + gn + e, cs[e]);
+        for (int e = 0; e < 8; ++e) atomicAdd(p.colsum + gn + e, cs[e]);
+      }
     }
   }
 }
@@ -831,6 +857,9 @@ int dispatch_e(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStrea
     case EPI_GATE_RESID: return dispatch_t<BM, BN, EPI_GATE_RESID, false>(p, at, bt, batch, s);
     case EPI_DSILU: return dispatch_t<BM, BN, EPI_DSILU, false>(p, at, bt, batch, s);
     case EPI_AXPBY: return dispatch_t<BM, BN, EPI_AXPBY, false>(p, at, bt, batch, s);
+    case EPI_SCALE2:  // X X^T only: both operands k-contiguous
+      if (at || bt) break;
+      return launch<BM, BN, false, false, EPI_SCALE2, false>(p, batch, s);
   }
   owlk::set_error("gemm: unknown epilogue %d", epi);
   return 1;
@@ -870,6 +899,9 @@ int dispatch256(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStre
     case EPI_GATE_RESID: return dispatch256_t<EPI_GATE_RESID, false>(p, at, bt, batch, s);
     case EPI_DSILU: return dispatch256_t<EPI_DSILU, false>(p, at, bt, batch, s);
     case EPI_AXPBY: return dispatch256_t<EPI_AXPBY, false>(p, at, bt, batch, s);
+    case EPI_SCALE2:
+      if (at || bt) break;
+      return launch256<false, false, EPI_SCALE2, false>(p, batch, s);
   }
   owlk::set_error("gemm: unknown epilogue %d", epi);
   return 1;
@@ -980,18 +1012,58 @@ static long skinny_splits(long M, long N, long K, long batch, int c_f32, int epi
   return (K + kchunk - 1) / kchunk;
 }
 
-static long splitk_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
-                        float beta) {
+// Split-K plans (one function, shared by the launch and the workspace query):
+//   SKINNY  M <= 256 bf16 outputs with few 64^2 tiles (decode): partials + splitk_epi_k
+//   S256    fp32 weight gradients on 256^2 tiles: partials + splitk_reduce_k
+//   S128    fp32 long reductions that do not tile by 256 (e.g. proj_in dW, N = 128): 128^2 tiles,
+//           partials + splitk_reduce_k (fp32 atomics only without a workspace)
+enum SplitKind { SPLIT_NONE = 0, SPLIT_SKINNY, SPLIT_256, SPLIT_128 };
+struct SplitPlan {
+  int kind;
+  long splits, kchunk;
+};
+
+static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
+                            float beta) {
+  SplitPlan pl{SPLIT_NONE, 1, K};
+  auto chunk = [&](long sp) { return ((K + sp - 1) / sp + BK - 1) / BK * BK; };
   const long sk = skinny_splits(M, N, K, batch, c_f32, epi, beta);
-  if (sk > 1) return sk;
-  if (!fits256(M, N, K, a_trans, b_trans, c_f32, beta)) return 1;
+  if (sk > 1) {
+    pl.kchunk = chunk(sk);
+    pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
+    pl.kind = SPLIT_SKINNY;
+    return pl;
+  }
+  const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
-  if (!(c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && tiles256 < 1024))
-    return 1;
-  const long splits = pick_splits(tiles256, K);
-  if (splits <= 1) return 1;
-  const long kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
-  return (K + kchunk - 1) / kchunk;
+  if (fits256(M, N, K, a_trans, b_trans, c_f32, beta)) {
+    if (c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && tiles256 < 1024) {
+      const long sp = pick_splits(tiles256, K);
+      if (sp > 1) {
+        pl.kchunk = chunk(sp);
+        pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
+        pl.kind = SPLIT_256;
+        return pl;
+      }
+    }
+    if (tiles256 >= 256) return pl;
+  }
+  if (c_f32 && epi == EPI_STORE && (beta == 1.f || (beta == 0.f && batch == 1)) && K >= 8192 && tiles128 < 1024) {
+    long sp = (1024 + tiles128 - 1) / tiles128;
+    if (sp > K / 4096) sp = K / 4096;
+    if (sp > 1) {
+      pl.kchunk = chunk(sp);
+      pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
+      pl.kind = SPLIT_128;
+    }
+  }
+  return pl;
+}
+
+// workspace bytes of a plan's per-split partials (0: the plan does not split or cannot use them)
+static long split_ws_bytes(const SplitPlan& pl, long M, long N, long batch) {
+  if (pl.kind == SPLIT_NONE || (pl.kind == SPLIT_128 && batch != 1)) return 0;
+  return pl.splits * M * N * (long)sizeof(float);
 }
 
 static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
@@ -1011,7 +1083,9 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   OWLK_REQUIRE(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "gemm: operands must be 16-byte aligned");
   OWLK_REQUIRE(!c_f32 || epi == EPI_STORE, "gemm: fp32 output only with EPI_STORE");
   OWLK_REQUIRE(epi != EPI_GATE_RESID || (gate && resid && tpf > 0), "gemm: gate epilogue needs gate/resid/tpf");
-  OWLK_REQUIRE(!(epi == EPI_SILU || epi == EPI_DSILU || epi == EPI_AXPBY) || aux, "gemm: epilogue needs aux");
+  OWLK_REQUIRE(!(epi == EPI_SILU || epi == EPI_DSILU || epi == EPI_AXPBY || epi == EPI_SCALE2) || aux,
+               "gemm: epilogue needs aux");
+  OWLK_REQUIRE(epi != EPI_SCALE2 || (!a_trans && !b_trans), "gemm: SCALE2 epilogue needs k-contiguous operands");
   p.M = M; p.N = N; p.K = K;
   p.A = (const bf16*)A; p.lda = lda; p.sA = sA;
   p.B = (const bf16*)B; p.ldb = ldb; p.sB = sB;
@@ -1024,10 +1098,13 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   p.kchunk = K;
+  const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+  const long pws = split_ws_bytes(pl, M, N, batch);
+  const bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
   {
-    const long sk = skinny_splits(M, N, K, batch, c_f32, epi, beta);
-    if (sk > 1 && ws && ws_bytes >= sk * M * N * (long)sizeof(float) && (uintptr_t)ws % 16 == 0) {
-      p.kchunk = ((K + sk - 1) / sk + BK - 1) / BK * BK;
+    const long sk = pl.splits;
+    if (pl.kind == SPLIT_SKINNY && have_ws) {
+      p.kchunk = pl.kchunk;
       p.ws = (float*)ws;
       if (int e = dispatch_e<64, 64>(p, a_trans, b_trans, epi, c_f32, batch, s)) return e;
       const long work = M * (N / 8);
@@ -1040,17 +1117,15 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
       return owlk::check_launch("splitk_epi");
     }
   }
+  // split-K onto an fp32 output: partials into the caller's workspace + one fixed-order reduce
+  // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32
+  // atomics onto C, cleared first when beta = 0
+  static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
   if (fits256(M, N, K, a_trans, b_trans, c_f32, beta)) {
-    // split-K onto an fp32 output: partials into the caller's workspace + one fixed-order reduce
-    // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32
-    // atomics onto C, cleared first when beta = 0
-    static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
-    const long nsp = splitk_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+    const long nsp = pl.kind == SPLIT_256 ? pl.splits : 1;
     if (nsp > 1) {
-      const long splits = pick_splits(tiles256, K);
-      p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
-      const long need = nsp * M * N * (long)sizeof(float);
-      if (atomic_splitk || !ws || ws_bytes < need || (uintptr_t)ws % 16) {
+      p.kchunk = pl.kchunk;
+      if (atomic_splitk || !have_ws) {
         if (beta == 0.f)
           OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
                        "gemm: clearing the split-K output failed");
@@ -1068,27 +1143,38 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
     }
     if (tiles256 >= 256) return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
   }
-  // long reductions onto small outputs (weight gradients, K = tokens): 128x128 tiles, K split so
-  // the grid covers ~4 workgroups per CU; fp32 atomics onto a caller-zeroed (beta 1) or cleared (beta 0) C
-  if (c_f32 && epi == EPI_STORE && (beta == 1.f || (beta == 0.f && batch == 1)) && K >= 8192 && tiles128 < 1024) {
-    long splits = (1024 + tiles128 - 1) / tiles128;
-    if (splits > K / 4096) splits = K / 4096;
-    if (splits > 1) {
-      if (beta == 0.f) {  // the atomics add onto C: clear it first
-        OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
-                     "gemm: clearing the split-K output failed");
-        p.beta = 1.f;
-      }
-      p.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
-      return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
+  // long reductions onto small outputs (weight gradients, K = tokens) that do not tile by 256:
+  // 128x128 tiles, K split so the grid covers ~4 workgroups per CU; per-split partials + a
+  // fixed-order reduce with a workspace, else fp32 atomics onto a cleared (beta 0) or kept (beta 1) C
+  if (pl.kind == SPLIT_128) {
+    p.kchunk = pl.kchunk;
+    if (have_ws && !atomic_splitk) {
+      p.ws = (float*)ws;
+      if (int e = dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s)) return e;
+      const long work = M * (N / 4);
+      const unsigned grid = (unsigned)std::min<long>((work + 255) / 256, 2048);
+      hipLaunchKernelGGL(splitk_reduce_k, dim3(grid), dim3(256), 0, s, p.ws, (int)pl.splits, M, N, (float*)C, ldc,
+                         alpha, beta);
+      return owlk::check_launch("splitk_reduce");
     }
+    if (beta == 0.f) {  // the atomics add onto C: clear it first
+      OWLK_REQUIRE(hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) == hipSuccess,
+                   "gemm: clearing the split-K output failed");
+      p.beta = 1.f;
+    }
+    return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
   }
   // small outputs (per-frame modulation, Newton-Schulz) use 64x64 tiles to fill the chip
   if (tiles128 < 512) return dispatch_e<64, 64>(p, a_trans, b_trans, epi, c_f32, batch, s);
   return dispatch_e<128, 128>(p, a_trans, b_trans, epi, c_f32, batch, s);
 }
 
-extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* stream);
+extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* ws, long ws_bytes,
+                           void* stream);
+extern "C" long owlk_colsum_ws_bytes(long R, long N);
+
+// column-sum partials of the fused DSILU epilogue: [tiles_m * 2][N] fp32
+static long fused_colsum_bytes(long M, long N) { return ((M + 255) / 256) * 2 * N * (long)sizeof(float); }
 
 extern "C" int owlk_gemm(long M, long N, long K, long batch,
                          const void* A, long lda, long sA, int a_trans,
@@ -1102,17 +1188,30 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   OWLK_REQUIRE(!colsum || (batch == 1 && !c_f32), "gemm: colsum needs batch 1 and a bf16 output");
   GemmP p{};
   p.colsum_req = colsum;
+  if (colsum && ws && (uintptr_t)ws % 16 == 0 && ws_bytes >= fused_colsum_bytes(M, N)) p.cs_part = (float*)ws;
   if (int e = gemm_dispatch(p, M, N, K, batch, A, lda, sA, a_trans, B, ldb, sB, b_trans, C, ldc, sC, c_f32, epi,
                             alpha, beta, bias, aux, ldaux, sAux, gate, ldgate, sGate, tpf, resid, ldres, sRes, ws,
                             ws_bytes, stream))
     return e;
-  if (colsum && !p.colsum) return owlk_colsum(C, 0, M, N, ldc, colsum, stream);  // not fused by this kernel
+  if (colsum && p.colsum && p.cs_part)  // fused, deterministic: add the per-wave partial rows in order
+    return owlk::colsum_reduce(p.cs_part, (int)(((M + 255) / 256) * 2), N, colsum, (hipStream_t)stream);
+  if (colsum && !p.colsum)  // not fused by this kernel: a separate (workspace: deterministic) pass
+    return owlk_colsum(C, 0, M, N, ldc, colsum, ws, ws_bytes, stream);
   return 0;
 }
 
 extern "C" long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32,
                                        int epi, float beta) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
-  const long nsp = splitk_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
-  return nsp > 1 ? nsp * M * N * (long)sizeof(float) : 0;
+  return split_ws_bytes(split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta), M, N, batch);
+}
+
+extern "C" long owlk_gemm_ws_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
+                                   float beta, int colsum) {
+  long b = owlk_gemm_splitk_bytes(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+  if (colsum && M > 0 && N > 0) {
+    const long c = std::max(fused_colsum_bytes(M, N), owlk_colsum_ws_bytes(M, N));
+    b = std::max(b, c);
+  }
+  return b;
 }

@@ -3,7 +3,7 @@
 // owlk_muon_momentum: one pass per parameter group does what the reference spends three torch
 //   passes on (buf.lerp_(g, 1-m); g.lerp_(buf, m); torch.stack) plus the Frobenius-norm reduction
 //   of the Newton-Schulz prologue (sum of bf16(g')^2, muon.py:24-26): reads g and buf, writes buf
-//   and the stacked fp32 NS input, accumulates ||bf16(g')||^2 per matrix.
+//   and the stacked fp32 NS input, and the kNormParts partial sums of ||bf16(g')||^2 per matrix.
 // owlk_muon_apply: p = p * (1 - lr*wd) - lr*scale * u (muon.py:80-84, two torch passes) in one,
 //   reading u straight from the NS output layout (transposed when rows > cols, 64x64 LDS tiles).
 // Each launch takes up to kMaxT same-shaped matrices as a kernel-argument pointer table (grid.y).
@@ -65,11 +65,9 @@ __global__ __launch_bounds__(256) void muon_momentum_k(Ptrs P, long n, float m, 
     }
   }
   if (!sumsq) return;
-  acc = wave_sum(acc);
   __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sumsq + z, red[0] + red[1] + red[2] + red[3]);
+  acc = block_sum256(acc, red);
+  if (threadIdx.x == 0) sumsq[(long)z * kNormParts + blockIdx.x] = acc;  // partial, fixed slot
 }
 
 // u[z] is [rows, cols] (TR = 0, contiguous) or [cols, rows] (TR = 1, the NS iterate before the
@@ -222,8 +220,9 @@ extern "C" int owlk_muon_momentum(int count, float* const* g, float* const* buf,
       vec = vec && aligned16(P.a[i]) && aligned16(P.b[i]);
     }
     float* st = stack ? stack + (long)base * n : nullptr;
-    float* sq = sumsq ? sumsq + base : nullptr;
-    const dim3 grid(flat_blocks(vec ? n / 4 : n, k), (unsigned)k);
+    float* sq = sumsq ? sumsq + (long)base * kNormParts : nullptr;
+    // with the norm requested: exactly kNormParts blocks per matrix, one partial slot each
+    const dim3 grid(sumsq ? (unsigned)kNormParts : flat_blocks(vec ? n / 4 : n, k), (unsigned)k);
     if (vec)
       hipLaunchKernelGGL(muon_momentum_k<true>, grid, dim3(256), 0, s, P, n, momentum, nesterov, st, sq);
     else

@@ -18,6 +18,7 @@ _SIGS = {
     "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P, P, L,
                   P],
     "owlk_gemm_splitk_bytes": [L, L, L, L, I, I, I, I, F],
+    "owlk_gemm_ws_bytes": [L, L, L, L, I, I, I, I, F, I],
     "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
     "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
     "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],
@@ -37,16 +38,23 @@ _SIGS = {
     "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
     "owlk_unpatchify": [P, I, I, L, P, P],
     "owlk_mse": [P, P, L, F, P, P, I, P],
-    "owlk_colsum": [P, I, L, L, L, P, P],
+    "owlk_colsum_ws_bytes": [L, L],
+    "owlk_colsum": [P, I, L, L, L, P, P, L, P],
     "owlk_ns_normalize": [P, I, L, L, L, I, P, P, P],
     "owlk_ns_scale": [P, I, L, L, L, I, P, P, P],
+    "owlk_ns_iterate_ws_bytes": [L, L, L],
+    "owlk_ns_iterate": [P, L, L, L, I, F, F, F, P, L, P],
+    "owlk_newton_schulz_ws_bytes": [L, L, L],
+    "owlk_newton_schulz_bf16": [P, I, L, L, L, I, F, F, F, P, P, L, P],
     "owlk_muon_momentum": [I, P, P, L, F, I, P, P, P],
     "owlk_muon_apply": [I, P, P, L, L, I, F, F, P],
     "owlk_adamw": [I, P, P, P, P, P, F, F, F, F, F, F, F, P],
     "owlk_ema": [I, P, P, P, F, P],
 }
 
-_RESTYPES = {"owlk_gemm_splitk_bytes": ctypes.c_long}  # size queries; every other entry returns an int status
+# size queries; every other entry returns an int status
+_RESTYPES = {n: ctypes.c_long for n in ("owlk_gemm_splitk_bytes", "owlk_gemm_ws_bytes", "owlk_colsum_ws_bytes",
+                                        "owlk_ns_iterate_ws_bytes", "owlk_newton_schulz_ws_bytes")}
 
 _lib = None
 

@@ -7,10 +7,11 @@ import os
 import torch
 
 
-def synthetic_video_batch(cfg, batch_size, seed=1234, n_docs=1, device="cpu"):
-    """(vid [b,n,c,h,w] bf16, mouse [b,n,2] bf16, btn [b,n,n_buttons] bf16, doc_id [b,n] int64)."""
+def synthetic_video_batch(cfg, batch_size, seed=1234, n_docs=1, device="cpu", n_frames=None):
+    """(vid [b,n,c,h,w] bf16, mouse [b,n,2] bf16, btn [b,n,n_buttons] bf16, doc_id [b,n] int64);
+    n = n_frames (a loader's window_length) or the model's n_frames."""
     g = torch.Generator().manual_seed(seed)
-    n, c, s = cfg.n_frames, cfg.channels, cfg.sample_size
+    n, c, s = n_frames or cfg.n_frames, cfg.channels, cfg.sample_size
     vid = torch.randn(batch_size, n, c, s, s, generator=g).to(torch.bfloat16)
     mouse = torch.randn(batch_size, n, 2, generator=g).to(torch.bfloat16)
     btn = (torch.rand(batch_size, n, cfg.n_buttons, generator=g) < 0.5).to(torch.bfloat16)
@@ -44,7 +45,8 @@ def get_loader(data_id, batch_size, model_cfg=None, n_batches=10 ** 9, **kwargs)
         return latent_seq_packing.get_loader(batch_size, **kwargs)
     if data_id in ("synthetic", "sequence_packing", "cod", "synthetic_video"):
         return SyntheticLoader(lambda i: synthetic_video_batch(model_cfg, batch_size, seed=1234 + i,
-                                                               n_docs=kwargs.get("n_docs", 1)), n_batches)
+                                                               n_docs=kwargs.get("n_docs", 1),
+                                                               n_frames=kwargs.get("window_length")), n_batches)
     if data_id in ("synthetic_audio", "local_waveform"):
         return SyntheticLoader(lambda i: synthetic_audio_batch(model_cfg, batch_size, seed=1234 + i), n_batches)
     raise NotImplementedError(f"data_id {data_id!r}: only synthetic latents are supported on this build "

@@ -6,12 +6,13 @@ operand its grid does not cover) and enqueues on torch's current HIP stream.
 import os
 
 import torch
+from torch.autograd.graph import increment_version
 
 from ._lib import call, lib, ptr, stream
 
 BF16, F32 = torch.bfloat16, torch.float32
 
-EPI_STORE, EPI_SILU, EPI_GATE_RESID, EPI_DSILU, EPI_AXPBY = 0, 1, 2, 3, 4
+EPI_STORE, EPI_SILU, EPI_GATE_RESID, EPI_DSILU, EPI_AXPBY, EPI_SCALE2 = 0, 1, 2, 3, 4, 5
 
 
 def _rowmajor(t, name):
@@ -46,12 +47,13 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
     if colsum is not None:
         assert colsum.dtype == F32 and colsum.numel() == N and colsum.is_contiguous() and not out_f32
     tile = 64 if ((M + 127) // 128) * ((N + 127) // 128) < 512 else 128
-    # split-K weight gradients: the workspace for the per-split partials comes from torch's caching
-    # allocator (the library never allocates); stream order keeps it alive for the launch
+    # split-K partials (weight gradients, skinny-M decode) and column-sum partials: the workspace of
+    # the deterministic form comes from torch's caching allocator (the library never allocates);
+    # stream order keeps it alive for the launch
     ws, ws_bytes = None, 0
-    if (out_f32 and K >= 8192) or (M <= 256 and K >= 512 and not out_f32):  # dW / skinny-M (decode) split-K
-        ws_bytes = lib().owlk_gemm_splitk_bytes(M, N, K, 1, int(a_trans), int(b_trans), int(out_f32), epi,
-                                                float(beta))
+    if (out_f32 and K >= 8192) or (M <= 256 and K >= 512 and not out_f32) or colsum is not None:
+        ws_bytes = lib().owlk_gemm_ws_bytes(M, N, K, 1, int(a_trans), int(b_trans), int(out_f32), epi, float(beta),
+                                            int(colsum is not None))
         if ws_bytes > 0:
             ws = torch.empty(ws_bytes, device=A.device, dtype=torch.uint8)
     call("owlk_gemm", M, N, K, 1,
@@ -304,12 +306,19 @@ def mse(pred, tgt, want_grad=True, grad_scale=1.0):
 
 
 def colsum(x, out=None):
-    """fp32 column sums of a 2-D row-major view."""
+    """fp32 column sums of a 2-D row-major view, added onto out (deterministic: row-split partials
+    in a workspace, summed in order)."""
     R, N = x.shape
     if out is None:
         out = torch.zeros(N, device=x.device, dtype=F32)
-    call("owlk_colsum", ptr(x), int(x.dtype == F32), R, N, x.stride(0), ptr(out), stream())
+    nb = lib().owlk_colsum_ws_bytes(R, N)
+    ws = torch.empty(nb, device=x.device, dtype=torch.uint8)
+    call("owlk_colsum", ptr(x), int(x.dtype == F32), R, N, x.stride(0), ptr(out), ptr(ws), nb, stream(),
+         key="owlk_colsum")
     return out
+
+
+NORM_PARTS = 256  # OWLK_NORM_PARTS: per-matrix partial sums of the Frobenius norm (fixed-order reduce)
 
 
 def ns_normalize(g, transpose, work=None):
@@ -317,19 +326,56 @@ def ns_normalize(g, transpose, work=None):
     b, r, c = g.shape
     x = torch.empty(b, c, r, device=g.device, dtype=BF16) if transpose else torch.empty(b, r, c, device=g.device,
                                                                                         dtype=BF16)
-    work = torch.empty(b, device=g.device, dtype=F32) if work is None else work
+    work = torch.empty(b, NORM_PARTS, device=g.device, dtype=F32) if work is None else work
+    assert work.dtype == F32 and work.numel() >= b * NORM_PARTS
     g = g.contiguous()
     call("owlk_ns_normalize", ptr(g), int(g.dtype == F32), r, c, b, int(transpose), ptr(x), ptr(work), stream())
     return x
 
 
-def ns_scale(g, transpose, sumsq):
-    """owlk_ns_normalize's scale pass given sumsq[b] = sum(bf16(g)^2) (from muon_momentum)."""
+def ns_scale(g, transpose, sumsq, out=None):
+    """owlk_ns_normalize's scale pass given sumsq [b, NORM_PARTS], the partial sums of sum(bf16(g)^2)
+    that muon_momentum writes."""
     b, r, c = g.shape
-    assert g.is_contiguous() and sumsq.dtype == F32 and sumsq.numel() == b
-    x = torch.empty((b, c, r) if transpose else (b, r, c), device=g.device, dtype=BF16)
+    assert g.is_contiguous() and sumsq.dtype == F32 and sumsq.shape == (b, NORM_PARTS) and sumsq.is_contiguous()
+    x = torch.empty((b, c, r) if transpose else (b, r, c), device=g.device, dtype=BF16) if out is None else out
+    assert x.shape == ((b, c, r) if transpose else (b, r, c)) and x.is_contiguous() and x.dtype == BF16
     call("owlk_ns_scale", ptr(g), int(g.dtype == F32), r, c, b, int(transpose), ptr(x), ptr(sumsq), stream())
     return x
+
+
+NS_COEFFS = (3.4445, -4.7750, 2.0315)  # muon.py:23
+
+
+def ns_iterate(x, steps, coeffs=NS_COEFFS):
+    """owlk_ns_iterate: the quintic iterations in place on a normalised bf16 X [b, m, k] (m <= k)."""
+    b, m, k = x.shape
+    assert x.dtype == BF16 and x.is_contiguous() and m <= k
+    nb = lib().owlk_ns_iterate_ws_bytes(b, m, k)
+    ws = torch.empty(nb, device=x.device, dtype=torch.uint8)
+    call("owlk_ns_iterate", ptr(x), b, m, k, int(steps), *(float(v) for v in coeffs), ptr(ws), nb, stream(),
+         key=f"ns_iterate[{b}x{m}x{k}]", flops=lambda: steps * b * (4.0 * m * m * k + 2.0 * m ** 3))
+    return x
+
+
+def newton_schulz(g, steps=5, coeffs=NS_COEFFS):
+    """owlk_newton_schulz_bf16: g [b, r, c] fp32 / bf16 -> bf16 [b, r, c] (muon.py:11-38 in one entry)."""
+    b, r, c = g.shape
+    g = g.contiguous()
+    assert g.dtype in (F32, BF16)
+    out = torch.empty(b, r, c, device=g.device, dtype=BF16)
+    nb = lib().owlk_newton_schulz_ws_bytes(b, r, c)
+    ws = torch.empty(nb, device=g.device, dtype=torch.uint8)
+    call("owlk_newton_schulz_bf16", ptr(g), int(g.dtype == F32), b, r, c, int(steps), *(float(v) for v in coeffs),
+         ptr(out), ptr(ws), nb, stream())
+    return out
+
+
+def _written(ts):
+    """In-place writes made through raw pointers are invisible to autograd's version counters:
+    bump them, so that every version-keyed cache (the bf16 weight copies of nn/fused.py) and
+    saved-tensor check sees the new values."""
+    increment_version(list(ts))
 
 
 def _ptr_array(ts):
@@ -338,15 +384,17 @@ def _ptr_array(ts):
 
 
 def muon_momentum(grads, bufs, momentum, nesterov, stack, sumsq):
-    """Fused buf.lerp_(g, 1-m); g' = lerp(g, buf, m) (or buf); stack[i] = g'; sumsq[i] += |bf16 g'|^2.
-    grads / bufs: same-numel fp32 contiguous tensors; stack fp32 [len, numel]; sumsq fp32 [len] (zeroed)."""
+    """Fused buf.lerp_(g, 1-m); g' = lerp(g, buf, m) (or buf); stack[i] = g'; sumsq[i] = the NORM_PARTS
+    partial sums of |bf16 g'|^2 (their sum is the squared norm).  grads / bufs: same-numel fp32
+    contiguous tensors; stack fp32 [len, numel]; sumsq fp32 [len, NORM_PARTS] (fully written)."""
     n = grads[0].numel()
     for t in list(grads) + list(bufs):
         assert t.dtype == F32 and t.is_contiguous() and t.numel() == n and t.is_cuda
     assert stack.dtype == F32 and stack.is_contiguous() and stack.shape == (len(grads), n)
-    assert sumsq.dtype == F32 and sumsq.numel() == len(grads)
+    assert sumsq.dtype == F32 and sumsq.shape == (len(grads), NORM_PARTS) and sumsq.is_contiguous()
     call("owlk_muon_momentum", len(grads), _ptr_array(grads), _ptr_array(bufs), n, float(momentum),
          int(bool(nesterov)), ptr(stack), ptr(sumsq), stream())
+    _written(bufs)
 
 
 def muon_apply(params, u, rows, cols, transpose, decay, alpha):
@@ -357,6 +405,7 @@ def muon_apply(params, u, rows, cols, transpose, decay, alpha):
     assert u.dtype == BF16 and u.is_contiguous() and u.numel() == len(params) * rows * cols
     call("owlk_muon_apply", len(params), _ptr_array(params), ptr(u), rows, cols, int(bool(transpose)), float(decay),
          float(alpha), stream())
+    _written(params)
 
 
 def adamw(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, weight_decay, eps, step):
@@ -373,6 +422,7 @@ def adamw(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, weight_decay, 
     call("owlk_adamw", len(params), _ptr_array(params), _ptr_array(grads), _ptr_array(exp_avgs),
          _ptr_array(exp_avg_sqs), (ctypes.c_long * len(ns))(*ns), float(lr), float(beta1), float(beta2),
          float(weight_decay), float(eps), float(step_size), float(bc2s), stream())
+    _written(list(params) + list(exp_avgs) + list(exp_avg_sqs))
 
 
 def ema_lerp(shadow, params, weight):
@@ -385,6 +435,7 @@ def ema_lerp(shadow, params, weight):
     ns = [t.numel() for t in shadow]
     call("owlk_ema", len(shadow), _ptr_array(shadow), _ptr_array(params), (ctypes.c_long * len(ns))(*ns),
          float(weight), stream())
+    _written(shadow)
 
 
 # ---------------------------------------------------------------- MMDiT plumbing (frames.hip)

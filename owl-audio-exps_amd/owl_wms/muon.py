@@ -1,18 +1,22 @@
 """Muon + AdamW (reference: owl_wms/muon.py:11-179) with Newton-Schulz on libowlk.
 
-``zeropower_via_newtonschulz5`` keeps the reference signature.  Same-shape parameters are
-orthogonalised as one batch (one set of batched GEMM launches per shape group instead of one
-per parameter): X = bf16(G)/(||X||_F+eps) (owlk_ns_normalize, transposed when rows > cols),
-then per iteration A = X X^T, B = b A + c A A, X = a X + B X on bf16 MFMA GEMMs whose AXPBY
-epilogue applies the scalar combination in bf16 exactly as the eager reference rounds it.
+``zeropower_via_newtonschulz5`` keeps the reference signature and runs as one library entry
+(owlk_newton_schulz_bf16): X = bf16(G)/(||X||_F+eps), transposed when rows > cols, then per
+iteration A = X X^T, B = b A + (c A) A, X = a X + B X on bf16 MFMA GEMMs, rounded in the eager
+reference's order (the A GEMM also emits bf16(c A); the other two apply the scalar
+combination in their AXPBY epilogue).
 
-Momentum + Nesterov + stacking + the Frobenius norm are one fused pass per shape group
-(owlk_muon_momentum), and decoupled weight decay + the scaled update another (owlk_muon_apply),
-reading the NS iterate in its transposed layout.
+Inside Muon.step, same-shape parameters are orthogonalised as one batch: momentum + Nesterov +
+stacking + the Frobenius norm are one fused pass per shape (owlk_muon_momentum), then the scale
+pass (owlk_ns_scale) and the batched iterations (owlk_ns_iterate); decoupled weight decay + the
+scaled update is another fused pass (owlk_muon_apply) reading the NS iterate in its transposed
+layout.
 
-Distributed (muon.py:86-115): NS work is dealt round-robin over ranks by parameter index and
-the bf16 updates are exchanged with all_gather_into_tensor (RCCL over xGMI on MI355X); every
-rank then applies every update, so replicas stay bit-identical.
+Distributed (muon.py:86-115): NS work is dealt round-robin over ranks by parameter index.  Each
+rank orthogonalises all the parameters it owns in a group as shape batches, then ONE bf16
+all_gather_into_tensor per parameter group exchanges them (RCCL over xGMI, async_op=True, so the
+gather of a group overlaps the next group's NS); every rank then applies every update, so
+replicas stay bit-identical.
 """
 import torch
 import torch.distributed as dist
@@ -22,7 +26,7 @@ from torch.optim.optimizer import Optimizer
 
 from . import kernels as K
 
-NS_A, NS_B, NS_C = 3.4445, -4.7750, 2.0315
+NS_A, NS_B, NS_C = K.NS_COEFFS
 
 
 def _pad8(G: Tensor) -> Tensor:
@@ -33,35 +37,35 @@ def _pad8(G: Tensor) -> Tensor:
     return torch.nn.functional.pad(G, (0, pc, 0, pr)) if (pr or pc) else G
 
 
-def _ns_iterate(X: Tensor, steps: int) -> Tensor:
-    """Quintic iterations on a normalised bf16 X [b, m, k] (m <= k); returns the final iterate."""
-    b, m, _ = X.shape
-    A = torch.empty(b, m, m, device=X.device, dtype=torch.bfloat16)
-    Bm = torch.empty_like(A)
-    X2 = torch.empty_like(X)
-    for _ in range(steps):
-        K.bgemm(X, X, A)                                                      # A = X X^T
-        K.bgemm(A, A, Bm, epi=K.EPI_AXPBY, alpha=NS_C, beta=NS_B, aux=A)      # B = b A + c A A
-        K.bgemm(Bm, X, X2, b_trans=True, epi=K.EPI_AXPBY, alpha=1.0, beta=NS_A, aux=X)  # X = a X + B X
-        X, X2 = X2, X
-    return X
-
-
 def newton_schulz_bf16(G: Tensor, steps: int = 5) -> Tensor:
     """G [b, r, c] (fp32 or bf16, on the GPU) -> bf16 [b, r, c] quintic NS orthogonalisation."""
     assert G.dim() == 3
-    b, r, c = G.shape
-    tr = r > c
-    X = _ns_iterate(K.ns_normalize(_pad8(G), tr), steps)
-    X = X.transpose(1, 2) if tr else X
-    return X[:, :r, :c] if X.shape[1:] != (r, c) else X
+    return K.newton_schulz(G, steps)
 
 
 def momentum_update(grads, bufs, momentum, nesterov, out, sumsq):
     """muon.py:67-73 for same-numel fp32 grads, fused (owlk_muon_momentum): bufs updated in place,
-    the Nesterov-combined gradients written to out [len, numel] (not back into p.grad), sumsq[i] +=
-    ||bf16(g'_i)||^2."""
+    the Nesterov-combined gradients written to out [len, numel] (not back into p.grad), sumsq[i] =
+    the partial sums of ||bf16(g'_i)||^2 [len, K.NORM_PARTS]."""
     K.muon_momentum(grads, bufs, momentum, nesterov, out, sumsq)
+
+
+def ns_orthogonalize(G: Tensor, sumsq: Tensor, steps: int, out: Tensor = None):
+    """muon.py:23-34 on a batch of momentum-combined fp32 matrices G [n, r, c] whose sum(bf16(g)^2)
+    partials are already in sumsq [n, K.NORM_PARTS]: -> (U, tr), U bf16 contiguous [n, c, r] when tr (the iterate before its
+    transpose back, r > c) else [n, r, c]; written into `out` when given (same shape)."""
+    n, r, c = G.shape
+    tr = r > c
+    Gp = _pad8(G)
+    if Gp is G and out is not None:
+        return K.ns_iterate(K.ns_scale(G, tr, sumsq, out=out), steps), tr
+    X = K.ns_iterate(K.ns_scale(Gp.contiguous(), tr, sumsq), steps)
+    if Gp is not G:  # zero-padded matrix: crop
+        X = (X[:, :c, :r] if tr else X[:, :r, :c]).contiguous()
+    if out is not None:
+        out.copy_(X)
+        X = out
+    return X, tr
 
 
 def apply_update(params, u, rows, cols, transpose, decay, alpha):
@@ -76,12 +80,27 @@ def zeropower_via_newtonschulz5(G: Tensor, steps: int) -> Tensor:
     return out.reshape(shp)
 
 
-def _all_gather(out, inp):
-    """all_gather_into_tensor (RCCL); list form where the backend lacks it (gloo tests)."""
+def _all_gather_async(out, inp):
+    """all_gather_into_tensor(async_op=True) (RCCL); list form where the backend lacks it (gloo)."""
     if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(out, inp)
-    else:
-        dist.all_gather(list(out.unbind(0)), inp)
+        return dist.all_gather_into_tensor(out, inp, async_op=True)
+    return dist.all_gather(list(out.view(dist.get_world_size(), -1).unbind(0)), inp, async_op=True)
+
+
+def _shape2(p):
+    return p.shape[0], p[0].numel()
+
+
+def _runs(items, key):
+    """consecutive runs of items with equal key -> [(key, [items])]"""
+    out = []
+    for it in items:
+        k = key(it)
+        if out and out[-1][0] == k:
+            out[-1][1].append(it)
+        else:
+            out.append((k, [it]))
+    return out
 
 
 class Muon(torch.optim.Optimizer):
@@ -96,7 +115,9 @@ class Muon(torch.optim.Optimizer):
         defaults = dict(lr=lr, weight_decay=weight_decay, momentum=momentum, nesterov=nesterov, ns_steps=ns_steps)
         params = [*params]
         groups = []
-        for size in sorted({p.numel() for p in params}):
+        # the reference iterates a set of numels (muon.py:52): same group order, so that a reference
+        # Muon state_dict loads onto the same parameters
+        for size in {p.numel() for p in params}:
             groups.append(dict(params=[p for p in params if p.numel() == size]))
         super().__init__(groups, defaults)
 
@@ -113,55 +134,65 @@ class Muon(torch.optim.Optimizer):
     def _scales(group, rows, cols):
         return 1 - group["lr"] * group["weight_decay"], group["lr"] * max(1, rows / cols) ** 0.5
 
+    def _orthogonalize(self, group, ps, out=None):
+        """momentum + NS for same-shape params ps (one batch) -> (U, tr) as ns_orthogonalize"""
+        for p in ps:  # the fused passes take flat fp32 storage
+            if not p.grad.is_contiguous():
+                p.grad = p.grad.contiguous()
+        r, c = _shape2(ps[0])
+        G = torch.empty(len(ps), r * c, device=ps[0].device, dtype=torch.float32)
+        sumsq = torch.empty(len(ps), K.NORM_PARTS, device=G.device, dtype=torch.float32)
+        momentum_update([p.grad for p in ps], self._buffers(ps), group["momentum"], group["nesterov"], G, sumsq)
+        return ns_orthogonalize(G.view(len(ps), r, c), sumsq, group["ns_steps"], out=out)
+
     @torch.no_grad()
     def step(self):
+        pending = []
         for group in self.param_groups:
-            params = [p for p in group["params"] if p.grad is not None]
-            if not params:
-                continue
-            for p in params:  # the fused passes take flat fp32 storage
-                if not p.grad.is_contiguous():
-                    p.grad = p.grad.contiguous()
             if self.world_size == 1:
-                # all same-shape parameters of the group as one batch: one momentum pass (which also
-                # stacks the NS input and reduces its norm), one NS launch sequence, one apply pass
+                params = [p for p in group["params"] if p.grad is not None]
                 by_shape = {}
                 for p in params:
-                    by_shape.setdefault((p.grad.shape[0], p.grad[0].numel()), []).append(p)
+                    by_shape.setdefault(_shape2(p), []).append(p)
                 for (r, c), ps in by_shape.items():
-                    G = torch.empty(len(ps), r * c, device=ps[0].device, dtype=torch.float32)
-                    sumsq = torch.zeros(len(ps), device=G.device, dtype=torch.float32)
-                    momentum_update([p.grad for p in ps], self._buffers(ps), group["momentum"], group["nesterov"],
-                                    G, sumsq)
-                    tr = r > c
-                    X = _ns_iterate(K.ns_scale(_pad8(G.view(len(ps), r, c)).contiguous(), tr, sumsq),
-                                    group["ns_steps"])
-                    if X.shape[1:] != ((c, r) if tr else (r, c)):  # zero-padded matrix: crop first
-                        X = (X.transpose(1, 2) if tr else X)[:, :r, :c].contiguous()
-                        tr = False
+                    U, tr = self._orthogonalize(group, ps)
                     decay, alpha = self._scales(group, r, c)
-                    apply_update(ps, X, r, c, tr, decay, alpha)
+                    apply_update(ps, U, r, c, tr, decay, alpha)
                 continue
-            # multi-rank: round-robin NS + all_gather of the flat bf16 updates (muon.py:86-115)
-            numel = params[0].numel()
-            ws = self.world_size
-            buf = torch.empty(ws, numel, device=params[0].device, dtype=torch.bfloat16)
-            for base in range(0, len(params), ws):
-                chunk = params[base:base + ws]
-                if self.rank < len(chunk):
-                    p = chunk[self.rank]
-                    r = p.grad.shape[0]
-                    G = torch.empty(1, numel, device=p.device, dtype=torch.float32)
-                    sumsq = torch.zeros(1, device=p.device, dtype=torch.float32)
-                    momentum_update([p.grad], self._buffers([p]), group["momentum"], group["nesterov"], G, sumsq)
-                    mine = newton_schulz_bf16(G.view(1, r, numel // r), group["ns_steps"])[0].flatten()
-                else:
-                    mine = torch.zeros(numel, device=buf.device, dtype=torch.bfloat16)
-                _all_gather(buf, mine.contiguous())
-                for i, p in enumerate(chunk):
-                    r = p.shape[0]
-                    decay, alpha = self._scales(group, p.size(-2), p.size(-1))
-                    apply_update([p.data], buf[i], r, numel // r, False, decay, alpha)
+            pending.append(self._launch_group(group))
+        for finish in pending:
+            finish()
+
+    def _launch_group(self, group):
+        """multi-rank (muon.py:86-115): NS of the params this rank owns (index % world_size == rank)
+        as shape batches into slot j of a [chunks, numel] bf16 buffer, then one async all_gather of
+        it; returns the closure that waits and applies every rank's updates."""
+        params, ws, rank = group["params"], self.world_size, self.rank
+        numel = params[0].numel()
+        nc = (len(params) + ws - 1) // ws
+        dev = params[0].device
+        mine = torch.zeros(nc, numel, device=dev, dtype=torch.bfloat16)
+        owned = [(j, params[j * ws + rank]) for j in range(nc) if j * ws + rank < len(params)]
+        for p in params:
+            assert p.grad is not None
+        for (r, c), run in _runs(owned, lambda jp: _shape2(jp[1])):
+            j0 = run[0][0]
+            slots = mine[j0:j0 + len(run)]  # owned params take consecutive slots j
+            tr = r > c
+            self._orthogonalize(group, [p for _, p in run], out=slots.view(len(run), *((c, r) if tr else (r, c))))
+        out = torch.empty(ws, nc, numel, device=dev, dtype=torch.bfloat16)
+        work = _all_gather_async(out.view(-1), mine.view(-1))
+
+        def finish():
+            work.wait()
+            for src in range(ws):
+                ps = [(j, params[j * ws + src]) for j in range(nc) if j * ws + src < len(params)]
+                for (r, c), run in _runs(ps, lambda jp: _shape2(jp[1])):
+                    j0 = run[0][0]
+                    decay, alpha = self._scales(group, r, c)
+                    apply_update([p for _, p in run], out[src, j0:j0 + len(run)], r, c, r > c, decay, alpha)
+
+        return finish
 
 
 class FusedAdamW(AdamW):

@@ -17,7 +17,15 @@
 
 Parameters stay fp32 (the reference trains fp32 master weights under autocast); their bf16
 copies are cached on the parameter and refreshed only when its version counter moves (i.e.
-after an optimizer step), not once per micro-step.
+after an optimizer step -- the fused optimizer passes bump it, kernels._written), not once per
+micro-step.
+
+Weight and bias gradients go straight into the parameter's gradient buffer when that buffer is a
+GradReducer bucket view (zeroed once per optimizer step): the dW GEMMs run with beta = 1 onto it
+and the bias column sums add onto it, the backward returns None for the parameter, and the
+reducer is told the gradient is complete.  That replaces autograd's separate fp32
+``p.grad += g`` pass per parameter per micro-step.  It needs each parameter used once per
+forward, which holds for every module on this path.
 """
 import weakref
 
@@ -43,6 +51,44 @@ def bf16_weight(p, pad_k=0):
     return ent[2]
 
 
+def grad_sink(p):
+    """p's GradReducer bucket view when the backward may accumulate into it directly, else None."""
+    if p is None or not p.requires_grad:
+        return None
+    v = getattr(p, "_owl_grad_view", None)
+    g = p.grad
+    if v is None or g is None or g.data_ptr() != v.data_ptr():
+        return None
+    return v
+
+
+def grad_done(p):
+    """the direct write into p's bucket view is enqueued: tell the reducer (bucket readiness)."""
+    r = getattr(p, "_owl_reducer", None)
+    if r is not None:
+        r.grad_ready(p)
+
+
+def wgrad_into(p, dy, x):
+    """weight gradient dW = dy^T x: accumulated into p's bucket view (returns None) or returned."""
+    sink = grad_sink(p)
+    if sink is None:
+        return K.gemm_wgrad(dy, x)
+    K.gemm(dy, x, a_trans=True, b_trans=True, out=sink, out_f32=True, beta=1.0)
+    grad_done(p)
+    return None
+
+
+def bgrad_into(p, dy):
+    """bias gradient sum_rows dy (bf16 or fp32 rows), accumulated into p's bucket view or returned."""
+    sink = grad_sink(p)
+    if sink is None:
+        return K.colsum(dy)
+    K.colsum(dy, out=sink)
+    grad_done(p)
+    return None
+
+
 def _pad_k(K_):
     return (-K_) % 8
 
@@ -61,6 +107,7 @@ class LinearFn(torch.autograd.Function):
         y = K.gemm(x2, wb, bias=b)
         ctx.save_for_backward(x2, w)
         ctx.pad, ctx.shp, ctx.has_b, ctx.xdtype = pad, shp, b is not None, x.dtype
+        ctx.bias = b
         return y.view(*shp[:-1], w.shape[0])
 
     @staticmethod
@@ -76,11 +123,12 @@ class LinearFn(torch.autograd.Function):
                 dx = dx[:, : ctx.shp[-1]]
             dx = dx.reshape(ctx.shp).to(ctx.xdtype)
         if ctx.needs_input_grad[1]:
-            dw = K.gemm_wgrad(dy2, x2)
             if ctx.pad:
-                dw = dw[:, : ctx.shp[-1]].contiguous()
+                dw = K.gemm_wgrad(dy2, x2)[:, : ctx.shp[-1]].contiguous()
+            else:
+                dw = wgrad_into(w, dy2, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = K.colsum(dy2)
+            db = bgrad_into(ctx.bias, dy2)
         return dx, dw, db
 
 
@@ -185,6 +233,7 @@ class DiTBlockFn(torch.autograd.Function):
         ctx.save_for_backward(xx, a1, gg1, a2, gg2, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2,
                               r2, a_pre, a, y2)
         ctx.geo, ctx.shape = geo, (B, T, d)
+        ctx.params = (wqkv, bqkv, wout, bout, w1, b1, w2, b2)
         return out.view(B, T, d)
 
     @staticmethod
@@ -197,13 +246,20 @@ class DiTBlockFn(torch.autograd.Function):
         H, D, tpf = geo.H, geo.D, geo.tpf
         dx2 = dout.reshape(M, d).to(BF16).contiguous()
 
+        prm = ctx.params  # (wqkv, bqkv, wout, bout, w1, b1, w2, b2) Parameters: direct gradient sinks
+
         # ---- MLP branch
         dy2, dg2, dbf2 = K.gate_bwd(dx2, y2, gg2, tpf)
-        db2 = dbf2.sum(0)
-        db1 = torch.zeros(a_pre.shape[1], device=a_pre.device, dtype=torch.float32)  # colsum(dapre), fused
-        dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=db1)
-        dw2 = K.gemm_wgrad(dy2, a)
-        dw1 = K.gemm_wgrad(dapre, h2)
+        db2 = bgrad_into(prm[7], dbf2)  # per-frame partials [F, d] -> bias gradient
+        sink_b1 = grad_sink(prm[5])
+        db1 = sink_b1 if sink_b1 is not None else torch.zeros(a_pre.shape[1], device=a_pre.device,
+                                                              dtype=torch.float32)
+        dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=db1)  # + colsum
+        if sink_b1 is not None:
+            grad_done(prm[5])
+            db1 = None
+        dw2 = wgrad_into(prm[6], dy2, a)
+        dw1 = wgrad_into(prm[4], dapre, h2)
         dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
         del dapre
         dx1, dmod2 = K.adaln_bwd(dh2, x1, r2, a2[:, :d], tpf, dres=dx2)
@@ -211,9 +267,9 @@ class DiTBlockFn(torch.autograd.Function):
 
         # ---- attention branch
         dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf)
-        dbout = dbf1.sum(0)
+        dbout = bgrad_into(prm[3], dbf1)
         do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
-        dwout = K.gemm_wgrad(dy1, o)
+        dwout = wgrad_into(prm[2], dy1, o)
         del dy1
         dqkv = torch.empty(M, 3 * d, device=xx.device, dtype=BF16)
         dqkr = torch.empty(M, 2 * d, device=xx.device, dtype=BF16)
@@ -224,8 +280,8 @@ class DiTBlockFn(torch.autograd.Function):
         del do
         K.qk_rope_bwd(dqkr, qkv, rq, H, D, geo.cos, geo.sin, dqkv, geo.tab_off, T)
         del dqkr
-        dbqkv = K.colsum(dqkv)
-        dwqkv = K.gemm_wgrad(dqkv, h1)
+        dbqkv = bgrad_into(prm[1], dqkv)
+        dwqkv = wgrad_into(prm[0], dqkv, h1)
         dh1 = K.gemm(dqkv, bf16_weight(wqkv), b_trans=True)
         del dqkv
         dx, dmod1 = K.adaln_bwd(dh1, xx, r1, a1[:, :d], tpf, dres=dx1)

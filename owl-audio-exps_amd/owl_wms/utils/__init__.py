@@ -38,3 +38,24 @@ def versatile_load(path):
     elif "model" in sd:
         sd = sd["model"]
     return strip_prefixes(sd)
+
+
+@torch.no_grad()
+def batch_permute(mouse, button, factor=1):
+    """utils/__init__.py:69-90: ``factor`` times, append a batch-permuted copy along time."""
+    for _ in range(factor):
+        inds = torch.randperm(mouse.size(0))
+        mouse = torch.cat([mouse, mouse.clone()[inds]], dim=1)
+        button = torch.cat([button, button.clone()[inds]], dim=1)
+    return mouse, button
+
+
+@torch.no_grad()
+def batch_permute_to_length(mouse, button, length):
+    """utils/__init__.py:93-118: double the controls by batch_permute until >= length, truncate."""
+    factor, n = 0, mouse.shape[1]
+    while n < length:
+        factor += 1
+        n *= 2
+    mouse, button = batch_permute(mouse, button, factor=factor)
+    return mouse[:, :length], button[:, :length]

@@ -4,7 +4,8 @@
   in place by autograd), so a ready bucket is all-reduced with no flatten/copy.
 * Buckets follow reverse parameter order (the order backward produces them) and are sized for
   xGMI rings (default 256 MB: 11 buckets for dit_v4's 2.82 GB of fp32 grads).
-* A post-accumulate-grad hook counts ready parameters; on the LAST micro-step of an
+* A post-accumulate-grad hook (or ``grad_ready`` from the fused backward, which writes dW / db
+  straight into the bucket views with beta = 1) counts ready parameters; on the LAST micro-step of an
   accumulation window a full bucket is launched immediately with ``async_op=True``: RCCL runs
   it on its own HIP stream (ordered after the producing kernels by RCCL's stream wait) while the
   backward of earlier layers continues on the compute stream.  Earlier micro-steps do not
@@ -42,11 +43,14 @@ class GradReducer:
                 self.bucket_of[p] = bi
                 p._owl_grad_view = buf[off:off + p.numel()].view_as(p)
                 off += p.numel()
+        for p in self.params:
+            p._owl_reducer = self  # the fused backward reports direct bucket writes (nn/fused.py grad_done)
         self.sync = False
         nccl = self.ws > 1 and dist.is_initialized() and dist.get_backend(self.pg) == "nccl"
         self.op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM  # RCCL averages in-collective
         self.pending = [0] * len(self.buckets)
         self.works = []
+        self.ready = set()
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
         self.zero_grad()
 
@@ -61,15 +65,22 @@ class GradReducer:
         self.sync = sync and self.ws > 1
         self.pending = [len(b) for b in self.buckets]
         self.works = []
+        self.ready = set()
         for p in self.params:  # autograd may have replaced grad if someone set it to None
             if p.grad is None or p.grad.data_ptr() != p._owl_grad_view.data_ptr():
                 if p.grad is not None:
                     p._owl_grad_view.copy_(p.grad)
                 p.grad = p._owl_grad_view
 
+    def grad_ready(self, p):
+        """p's gradient for this micro-step is complete in its bucket view (autograd's
+        post-accumulate hook, or a direct write by the fused backward)."""
+        self._hook(p)
+
     def _hook(self, p):
-        if not self.sync:
+        if not self.sync or p in self.ready:
             return
+        self.ready.add(p)
         bi = self.bucket_of[p]
         self.pending[bi] -= 1
         if self.pending[bi] == 0:
@@ -94,16 +105,43 @@ class GradReducer:
 
 
 class EMA:
-    """ema_pytorch.EMA(model, beta, update_after_step=0, update_every=1) restated (rft_trainer.py:105,
-    library absent offline: parity unpinned).  decay_t = min(beta, 1 - (1 + t)^(-2/3)), t = steps
-    after the first update (which copies the weights)."""
+    """ema_pytorch.EMA(model, beta, update_after_step=0, update_every=1) restated (rft_trainer.py:105;
+    the library is absent offline: parity unpinned, restated from its published algorithm).
+
+    ``ema_model`` is a frozen deep copy of the model (what the reference samples with,
+    rft_trainer.py:244); ``update()``: step s = self.step, then self.step += 1; skip unless
+    s % update_every == 0; copy the weights while s <= update_after_step; on the first update
+    after that copy them again and set ``initted``; then lerp every parameter toward the online
+    weights by 1 - decay, decay = clamp(1 - (1 + e / inv_gamma)^-power, 0, beta) with
+    e = max((s + 1) - update_after_step - 1, 0) (the counter is read after its increment; decay 0
+    at e = 0).  The lerp is one libowlk
+    multi-tensor pass (owlk_ema).  state_dict: 'initted', 'step' and 'ema_model.<param>' keys, the
+    ema_pytorch layout (so a reference checkpoint's 'ema' entry loads after prefix stripping)."""
 
     def __init__(self, model, beta=0.999, update_after_step=0, update_every=1, inv_gamma=1.0, power=2 / 3):
-        self.model = model
+        import copy
+        self.online = [model]  # not a submodule (ema_pytorch keeps it in a list too)
         self.beta, self.after, self.every, self.inv_gamma, self.power = beta, update_after_step, update_every, inv_gamma, power
+        self.ema_model = copy.deepcopy(model)
+        self.ema_model.requires_grad_(False)
         self.params = [p for p in model.parameters()]
-        self.shadow = [p.detach().clone() for p in self.params]
+        self.shadow = [p for p in self.ema_model.parameters()]
         self.step, self.initted = 0, False
+
+    @property
+    def model(self):
+        return self.online[0]
+
+    def _copy(self):
+        with torch.no_grad():
+            for s, p in zip(self.shadow, self.params):
+                s.copy_(p.detach())
+
+    def get_current_decay(self):
+        epoch = max(self.step - self.after - 1, 0)  # ema_pytorch reads the already-advanced step
+        if epoch <= 0:
+            return 0.0
+        return max(0.0, min(self.beta, 1 - (1 + epoch / self.inv_gamma) ** -self.power))
 
     @torch.no_grad()
     def update(self):
@@ -111,26 +149,23 @@ class EMA:
         self.step += 1
         if step % self.every != 0:
             return
-        if step <= self.after or not self.initted:
-            for s, p in zip(self.shadow, self.params):
-                s.copy_(p.detach())
-            self.initted = True
+        if step <= self.after:
+            self._copy()
             return
-        epoch = max(step - self.after - 1, 0)
-        decay = 0.0 if epoch <= 0 else min(self.beta, 1 - (1 + epoch / self.inv_gamma) ** -self.power)
+        if not self.initted:
+            self._copy()
+            self.initted = True
         from .. import kernels as K
-        K.ema_lerp(self.shadow, [p.detach() for p in self.params], 1.0 - decay)  # one libowlk pass (owlk_ema)
+        K.ema_lerp(self.shadow, [p.detach() for p in self.params], 1.0 - self.get_current_decay())
 
     def state_dict(self):
-        names = [n for n, _ in self.model.named_parameters()]
-        d = {"ema_model." + n: s for n, s in zip(names, self.shadow)}
-        d["initted"] = torch.tensor(self.initted)
-        d["step"] = torch.tensor(self.step)
+        d = {"initted": torch.tensor(self.initted), "step": torch.tensor(self.step)}
+        for k, v in self.ema_model.state_dict().items():
+            d["ema_model." + k] = v
         return d
 
-    def load_state_dict(self, d):
-        names = [n for n, _ in self.model.named_parameters()]
-        for n, s in zip(names, self.shadow):
-            s.copy_(d["ema_model." + n])
-        self.initted = bool(d.get("initted", True))
-        self.step = int(d.get("step", 0))
+    def load_state_dict(self, d, strict=True):
+        sd = {k[len("ema_model."):]: v for k, v in d.items() if k.startswith("ema_model.")}
+        self.ema_model.load_state_dict(sd, strict=strict)
+        self.initted = bool(d.get("initted", torch.tensor(True)))
+        self.step = int(d.get("step", torch.tensor(0)))

@@ -13,7 +13,8 @@ Recipe: SURVEY.md §8(c).  Shims supplied here (all our own code, no reference t
 Outputs are small .pt dicts (tensors / ints / floats / strings) loaded with weights_only=True.
 Parameters are NOT stored: they come from oracle/params.py's deterministic recipe.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # every fixture below
+    python tests/golden/make_golden.py d128     # gamerft_d128.pt only
 """
 import importlib.util
 import os
@@ -268,6 +269,42 @@ def gen_gamerft():
     return out
 
 
+def gen_d128():
+    """Head dim 128 (configs/dit_v4_5B.yml: d 2560 / 20 heads): MotionRoPE tables of the 5B config
+    (head / tail rows), the rotation at D = 128, and a tiny D = 128 GameRFT (d 256, 2 heads,
+    gradient_checkpointing as the 5B config) trained one fwd+bwd under bf16 autocast."""
+    out = {}
+    big = tiny_video_cfg(n_frames=1536, d_model=2560, n_heads=20)
+    rb = r_rope.MotionRoPE(big)
+    out["mrope.5b.cos.head"], out["mrope.5b.sin.head"] = rb.cos[:128].clone(), rb.sin[:128].clone()
+    out["mrope.5b.cos.tail"], out["mrope.5b.sin.tail"] = rb.cos[-128:].clone(), rb.sin[-128:].clone()
+    out["mrope.5b.shape"] = list(rb.cos.shape)
+    cfg = tiny_video_cfg(d_model=256, n_heads=2, gradient_checkpointing=True)
+    rope = r_rope.MotionRoPE(cfg)
+    xq = det_tensor((1, 2, 256, 128), 310)
+    out["rope128.x"], out["rope128.y"] = xq, rope(xq)
+    out["rope128.xb"], out["rope128.yb"] = xq.to(torch.bfloat16), rope(xq.to(torch.bfloat16))
+    model = det_init_(r_gamerft.GameRFT(cfg), base_seed=1100).train()
+    inp = video_inputs(cfg, 2, torch.bfloat16, seed=620)
+    with inject_rng(rand=[inp["rand_b"]], randn=[inp["ts_raw"]], randn_like=[inp["z"]]), \
+            torch.autocast("cpu", dtype=torch.bfloat16):
+        d = model(inp["x"], inp["mouse"], inp["btn"], inp["doc_id"], return_dict=True)
+        d["diffusion_loss"].backward()
+    p = "d128.bf16."
+    for k, v in inp.items():
+        out[p + "in." + k] = v
+    out[p + "loss"] = d["diffusion_loss"].detach().float()
+    out[p + "pred"] = d["pred_video"].detach().float()
+    out[p + "cfg_mask"] = d["cfg_mask"]
+    for i, (k, prm) in enumerate(sorted(model.named_parameters())):
+        out[p + "gradstat." + k] = proj_stats(prm.grad, 7500 + i)
+        if ".blocks.0.attn." in k or ".blocks.1.attn.qkv" in k or ".blocks.0.adaln1" in k or \
+                "proj_out.proj" in k or "proj_in" in k:
+            out[p + "grad." + k] = prm.grad.clone()
+    out["d128.schema"] = [[k, list(v.shape)] for k, v in model.state_dict().items()]
+    return out
+
+
 def gen_audio_traj():
     out = {}
     cfg = audio_cfg()
@@ -305,6 +342,12 @@ def gen_schema():
 
 def main():
     torch.manual_seed(0)
+    if sys.argv[1:] == ["d128"]:  # only the head-dim-128 fixture (added in round 2)
+        d = gen_d128()
+        torch.save(d, os.path.join(HERE, "gamerft_d128.pt"))
+        print("gamerft_d128.pt", os.path.getsize(os.path.join(HERE, "gamerft_d128.pt")) // 1024, "KiB",
+              "loss", d["d128.bf16.loss"].item())
+        return
     import json
     with open(os.path.join(HERE, "schema.json"), "w") as f:
         json.dump(gen_schema(), f)

@@ -76,6 +76,91 @@ def test_library_exports_every_header_symbol():
     assert declared == set(exported_symbols())
 
 
+def _header_protos():
+    """include/owlk.h prototypes -> {name: [kind per argument]}, kinds P (pointer), L, I, F."""
+    hdr = re.sub(r"/\*.*?\*/", " ", open(os.path.join(REPO, "include", "owlk.h")).read(), flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\b(?:const\s+)?(?:char|int|long|void)\s*\*?\s*(owlk_\w+)\s*\(([^)]*)\)\s*;", hdr):
+        kinds = []
+        for a in [x.strip() for x in m.group(2).split(",")]:
+            if a in ("", "void"):
+                continue
+            if "*" in a:
+                kinds.append("P")
+            else:
+                t = re.match(r"(?:const\s+)?(long|int|float)\b", a)
+                assert t, f"{m.group(1)}: unparsed argument {a!r}"
+                kinds.append({"long": "L", "int": "I", "float": "F"}[t.group(1)])
+        protos[m.group(1)] = kinds
+    return protos
+
+
+_KIND = {ctypes.c_void_p: "P", ctypes.c_long: "L", ctypes.c_int: "I", ctypes.c_float: "F"}
+
+
+def test_ctypes_signatures_match_header():
+    """Every _SIGS entry (the package's ctypes binding) equals its owlk.h prototype argument by
+    argument; every header prototype is bound."""
+    from owl_wms._lib import _SIGS
+    protos = _header_protos()
+    assert set(protos) - {"owlk_last_error", "owlk_version", "owlk_device_ok"} == set(_SIGS)
+    for name, args in _SIGS.items():
+        assert [_KIND[a] for a in args] == protos[name], name
+
+
+def test_integration_binding_matches_header(monkeypatch):
+    """The reference-side binding in INTEGRATION.md (owl_wms/nn/owlk_bind.py): its argtypes equal
+    the owlk.h prototypes, and its attn_fwd / newton_schulz5 pass exactly the header's arguments
+    (count and kind) -- run against a stand-in library, no GPU."""
+    protos = _header_protos()
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = [b for b in re.findall(r"```python\n(.*?)```", text, flags=re.S) if "ctypes.CDLL" in b]
+    assert len(block) == 1
+    calls = []
+
+    class Fn:
+        def __init__(self, name):
+            self.name, self.argtypes, self.restype = name, None, None
+
+        def __call__(self, *args):
+            kinds = protos[self.name]
+            assert len(args) == len(kinds), (self.name, len(args), len(kinds))
+            for a, k in zip(args, kinds):
+                if k == "P":
+                    assert a is None or isinstance(a, (ctypes.c_void_p, int)), (self.name, a)
+                elif k == "F":
+                    assert isinstance(a, (float, int)) and not isinstance(a, bool), (self.name, a)
+                else:
+                    assert isinstance(a, int) and not isinstance(a, bool), (self.name, a)
+            calls.append(self.name)
+            return 256 if self.name.endswith("_bytes") else 0
+
+    class Lib:
+        def __init__(self, *a, **k):
+            self.fns = {}
+
+        def __getattr__(self, name):
+            return self.fns.setdefault(name, Fn(name))
+
+    monkeypatch.setattr(ctypes, "CDLL", Lib)
+
+    class S:
+        cuda_stream = 0
+
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: S())
+    ns = {}
+    exec(compile(block[0], "INTEGRATION.md", "exec"), ns)
+    lib = ns["_L"]
+    for name, fn in lib.fns.items():
+        if fn.argtypes is not None:
+            assert [_KIND[a] for a in fn.argtypes] == protos[name], name
+    q = torch.zeros(1, 4, 2, 8, dtype=torch.bfloat16)
+    ns["attn_fwd"](q, q, q, tpf=2, window=None)
+    ns["attn_fwd"](q, q, q, tpf=2, window=3, score_bound=1.02 * 8)
+    ns["newton_schulz5"](torch.zeros(3, 16, 24), steps=5)
+    assert calls == ["owlk_attn_fwd", "owlk_attn_fwd", "owlk_newton_schulz_ws_bytes", "owlk_newton_schulz_bf16"]
+
+
 def _brute_arrays(doc, window):
     nf = doc.numel()
     kv_lo, q_hi = [], []
@@ -106,6 +191,11 @@ def test_frame_arrays_bruteforce(window):
 
 
 # ------------------------------------------------------------------ world_size 2 on gloo
+# one numel (96) in three shapes: the group mixes transposed (r > c) and plain NS layouts, and 5
+# params over 2 ranks leave the last chunk short
+MUON_SHAPES = [(8, 12), (8, 12), (12, 8), (12, 8), (8, 12)]
+
+
 def _worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
@@ -123,9 +213,8 @@ def _worker(rank, ws, port, q):
             red.finish()
         q.put((rank, [p.grad.numpy().copy() for p in model.parameters()], len(red.buckets)))
 
-        # distributed Muon: round-robin NS + all_gather_into_tensor, NS from the CPU oracle
+        # distributed Muon: round-robin NS + one async all_gather per group, NS from the CPU oracle
         import owl_wms.muon as mu
-        mu.newton_schulz_bf16 = lambda G, steps=5: torch.stack([R.newton_schulz5(x, steps) for x in G])
 
         # torch restatements of the fused HIP passes (muon.py:67-84) stand in for them on the CPU
         def _mom(grads, bufs, m, nesterov, out, sumsq):
@@ -133,14 +222,25 @@ def _worker(rank, ws, port, q):
                 b.lerp_(g, 1 - m)
                 out[i] = (g.lerp(b, m) if nesterov else b).flatten()
 
+        def _ns(G, sumsq, steps, out=None):
+            tr = G.shape[1] > G.shape[2]
+            U = torch.stack([R.newton_schulz5(x, steps) for x in G])
+            U = U.transpose(1, 2).contiguous() if tr else U  # the iterate's layout before its transpose back
+            if out is not None:
+                out.copy_(U)
+                U = out
+            return U, tr
+
         def _app(params, u, r, c, tr, decay, alpha):
             for i, p in enumerate(params):
-                p.mul_(decay).add_(u.view(len(params), r, c)[i].float(), alpha=-alpha)
+                ui = u.reshape(len(params), c, r)[i].T if tr else u.reshape(len(params), r, c)[i]
+                p.mul_(decay).add_(ui.float(), alpha=-alpha)
 
-        mu.momentum_update, mu.apply_update = _mom, _app
-        ps = [torch.nn.Parameter(torch.randn(8, 12, generator=torch.Generator().manual_seed(i))) for i in range(3)]
+        mu.momentum_update, mu.ns_orthogonalize, mu.apply_update = _mom, _ns, _app
+        ps = [torch.nn.Parameter(torch.randn(*MUON_SHAPES[i], generator=torch.Generator().manual_seed(i)))
+              for i in range(len(MUON_SHAPES))]
         for i, p in enumerate(ps):
-            p.grad = torch.randn(8, 12, generator=torch.Generator().manual_seed(50 + i))
+            p.grad = torch.randn(*MUON_SHAPES[i], generator=torch.Generator().manual_seed(50 + i))
         opt = mu.Muon(ps, lr=0.1, momentum=0.95, rank=rank, world_size=ws)
         opt.step()
         q.put((rank, "muon", [p.detach().numpy().copy() for p in ps]))
@@ -177,12 +277,12 @@ def test_reducer_and_muon_world_size_2():
     for a, b in zip(muon[0], muon[1]):
         assert torch.equal(a, b)  # replicas bit-identical after the gathered updates
     # and equal to the single-rank update
-    ps = [torch.randn(8, 12, generator=torch.Generator().manual_seed(i)) for i in range(3)]
+    ps = [torch.randn(*s, generator=torch.Generator().manual_seed(i)) for i, s in enumerate(MUON_SHAPES)]
     for i, p in enumerate(ps):
-        g = torch.randn(8, 12, generator=torch.Generator().manual_seed(50 + i))
+        g = torch.randn(*MUON_SHAPES[i], generator=torch.Generator().manual_seed(50 + i))
         g2 = g.lerp(torch.zeros_like(g).lerp(g, 0.05), 0.95)
         u = R.newton_schulz5(g2).float()
-        exp = p * (1 - 0.1 * 0.01) - 0.1 * max(1, 8 / 12) ** 0.5 * u
+        exp = p * (1 - 0.1 * 0.01) - 0.1 * max(1, p.shape[0] / p.shape[1]) ** 0.5 * u
         torch.testing.assert_close(muon[0][i], exp, rtol=1e-5, atol=1e-6)
 
 
@@ -338,3 +438,55 @@ def test_kv_cache_extend_matches_cat_model():
             assert torch.equal(k, ref[i][0]) and torch.equal(v, ref[i][1])
             assert c.length_at(i) == ref[i][0].shape[1]
     assert c.offsets == off
+
+
+def test_log_helper_semantics():
+    """utils/logging.py:33-64: per-key sums of value / world_size over the logged micro-steps
+    (the caller divides by accum); pop() clears.  Device tensors are summed without host syncs."""
+    from owl_wms.utils.logging import LogHelper
+    m = LogHelper()
+    for v in (torch.tensor(0.5), torch.tensor(0.25), 0.125):
+        m.log("diffusion_loss", v)
+    m.log_dict({"x": 2.0})
+    out = m.pop()
+    assert out == {"diffusion_loss": 0.875, "x": 2.0}
+    assert m.pop() == {}
+
+
+def test_strip_prefixes_model_and_ema_keys():
+    """rft_trainer.py:86-89: compiled / DDP prefixes stripped from model AND EMA keys."""
+    from owl_wms.utils import strip_prefixes
+    sd = {"_orig_mod.module.core.proj_in.weight": 1, "module.core.x": 2, "core.y": 3,
+          "ema_model._orig_mod.module.core.proj_in.weight": 4, "ema_model.module.core.z": 5, "initted": 6, "step": 7}
+    assert strip_prefixes(sd) == {"core.proj_in.weight": 1, "core.x": 2, "core.y": 3,
+                                  "ema_model.core.proj_in.weight": 4, "ema_model.core.z": 5, "initted": 6, "step": 7}
+
+
+def test_scheduler_registry():
+    """schedulers.py: the reference's factory is an empty stub; names resolve to torch LR schedulers,
+    anything else fails loudly at construction."""
+    from owl_wms.schedulers import get_scheduler_cls
+    assert get_scheduler_cls("LinearLR") is torch.optim.lr_scheduler.LinearLR
+    with pytest.raises(NotImplementedError):
+        get_scheduler_cls("warmup_cosine_custom")
+
+
+def test_muon_group_order_matches_reference():
+    """muon.py:52 iterates a set of numels: the param groups come out in that order (dit_v4: qkv,
+    out, fc), so a reference Muon state_dict loads onto the same parameters."""
+    from owl_wms.muon import Muon
+    numels = [(4608, 1536), (1536, 1536), (6144, 1536), (1536, 6144)] * 2 + [(3072, 1536)]
+    ps = [torch.nn.Parameter(torch.empty(s, device="meta")) for s in numels]
+    opt = Muon(ps, lr=1e-3, rank=0, world_size=1)
+    ref_order = list({p.numel() for p in ps})
+    assert [g["params"][0].numel() for g in opt.param_groups] == ref_order
+    assert ref_order[:3] == [7077888, 2359296, 9437184]  # the order the survey recorded for dit_v4
+
+
+def test_batch_permute_to_length():
+    """utils/__init__.py:69-118: controls doubled by batch permutation until long enough."""
+    from owl_wms.utils import batch_permute_to_length
+    m, b = torch.randn(4, 5, 2), torch.randn(4, 5, 11)
+    m2, b2 = batch_permute_to_length(m, b, 17)
+    assert m2.shape == (4, 17, 2) and b2.shape == (4, 17, 11)
+    assert torch.equal(m2[:, :5], m) and torch.equal(b2[:, :5], b)

@@ -172,8 +172,10 @@ def test_gate_bwd():
     assert rel(dbf, (dout.float() * gb).bfloat16().float().view(F, tpf, d).sum(1)) < 1e-4
 
 
-@pytest.mark.parametrize("D", [64])
+@pytest.mark.parametrize("D", [64, 128])
 def test_qk_rope(D):
+    """fused QK-RMSNorm + RoPE at dit_v4's head dim 64 and dit_v4_5B's 128 (MotionRoPE tables of
+    that head dim, rope.py:88-152; the oracle's tables are pinned to the reference's at both)."""
     k = K()
     H, T = 3, 256
     ang = R.motion_rope_angles(4, 8, D)
@@ -250,7 +252,7 @@ def test_attention_fwd_bwd(case, D):
     dq, dk, dv = (torch.empty_like(q) for _ in range(3))
     k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, dq, dk, dv)
     for got, ref in ((dq, qr.grad), (dk, kr.grad), (dv, vr.grad)):
-        assert rel(got.view(B, L, H, D).transpose(1, 2), ref) < 2e-2
+        assert rel(got.view(B, L, H, D).transpose(1, 2), ref) < 1e-2  # SURVEY §8(c) per-op
 
 
 @pytest.mark.parametrize("case,D", [(ATTN_CASES[0], 64), (ATTN_CASES[2], 64), (ATTN_CASES[4], 64), (ATTN_CASES[6], 64),
@@ -294,6 +296,103 @@ def test_attention_dit_v4_shape_smoke():
         assert (o.float() - 1).abs().max().item() < 1e-2  # softmax rows sum to one
 
 
+def _sample_rows(L, tpf, n, seed):
+    """edge rows (first / last token, frame and 128-row tile seams, the middle) plus random ones"""
+    fixed = [0, 1, tpf - 1, tpf, 127, 128, 4095, 4096, L // 2, L // 2 + tpf - 1, L - tpf, L - 1]
+    g = torch.Generator().manual_seed(seed)
+    extra = torch.randint(0, L, (n - len(fixed),), generator=g).tolist()
+    return torch.tensor(sorted(set(fixed + extra)), device=DEV)
+
+
+@pytest.mark.parametrize("window", [None, 16])
+def test_attention_bwd_dit_v4_shape_sampled_rows(window):
+    """The production shape (B 1 x H 24 x 98,304 tokens, tpf 64, global and window-16 layers, the
+    QK-RMSNorm'd inputs and score_bound of the model; attn.py:24-62, 106-109) through owlk_attn_fwd
+    and the two backward kernels -- every block of the XCD-aware remap and the 128-row tile paths
+    run as in the bench -- checked on sampled rows of four heads against fp32 torch: O and dQ of
+    sampled query rows over all their allowed keys; dK and dV of sampled key rows over all their
+    allowed queries (with fp32 lse and delta recomputed for every query of the head).  Tolerance:
+    rel-L2 <= 1e-2 (SURVEY §8(c) per-op) over the sampled rows."""
+    k = K()
+    B, H, nf, tpf, D = 1, 24, 1536, 64, 64
+    L = nf * tpf
+    gen = torch.Generator(device=DEV).manual_seed(11)
+
+    def unit(t):  # QK-RMSNorm (attn.py:84): |q.k| <= D, what score_bound promises
+        t = t.view(L, H, D)
+        return (t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True))).bfloat16().view(1, L, H * D)
+
+    q = unit(torch.randn(L, H * D, device=DEV, generator=gen))
+    kk = unit(torch.randn(L, H * D, device=DEV, generator=gen))
+    v = torch.randn(1, L, H * D, device=DEV, generator=gen).bfloat16()
+    do = torch.randn(1, L, H * D, device=DEV, generator=gen).bfloat16()
+    mask = k.FrameMask(tpf, window)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask, score_bound=k.qk_norm_bound(D))
+    dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+    k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, dq, dk, dv)
+    torch.cuda.synchronize()
+    scale = D ** -0.5
+    fr = torch.arange(L, device=DEV) // tpf
+
+    def allowed(qi, kj):  # frame mask predicate for index vectors
+        ok = fr[kj][None, :] <= fr[qi][:, None]
+        if window is not None:
+            ok &= fr[qi][:, None] - fr[kj][None, :] < window
+        return ok
+
+    def key_range(c0, c1):
+        lo = 0 if window is None else max(0, (c0 // tpf - window + 1) * tpf)
+        return lo, ((c1 - 1) // tpf + 1) * tpf
+
+    qrows, krows = _sample_rows(L, tpf, 16, 1), _sample_rows(L, tpf, 16, 2)
+    got, ref = {n: [] for n in ("o", "dq", "dk", "dv")}, {n: [] for n in ("o", "dq", "dk", "dv")}
+    for h in (0, 7, 13, 23):
+        cs = slice(h * D, (h + 1) * D)
+        qh, kh, vh, doh = (t[0, :, cs].float() for t in (q, kk, v, do))
+        lse_r = torch.empty(L, device=DEV)
+        o_r = torch.empty(L, D, device=DEV)
+        CH = 4096
+        for c0 in range(0, L, CH):
+            c1 = min(L, c0 + CH)
+            lo, hi = key_range(c0, c1)
+            s = (qh[c0:c1] @ kh[lo:hi].T) * scale
+            s.masked_fill_(~allowed(torch.arange(c0, c1, device=DEV), torch.arange(lo, hi, device=DEV)),
+                           float("-inf"))
+            lse_r[c0:c1] = torch.logsumexp(s, -1)
+            o_r[c0:c1] = torch.exp(s - lse_r[c0:c1, None]) @ vh[lo:hi]
+            del s
+        delta_r = (doh * o_r).sum(-1)
+        # lse is base 2 inside the kernels (lse2 = lse / ln 2)
+        assert (lse[0, h, qrows] * torch.log(torch.tensor(2.0)) - lse_r[qrows]).abs().max().item() < 2e-2
+        # sampled query rows: O, dQ over all allowed keys
+        for i in qrows.tolist():
+            lo, hi = key_range(i, i + 1)
+            kj = torch.arange(lo, hi, device=DEV)
+            ok = allowed(torch.tensor([i], device=DEV), kj)[0]
+            s = (qh[i] @ kh[lo:hi].T) * scale
+            p = torch.where(ok, torch.exp(s - lse_r[i]), torch.zeros_like(s))
+            dp = doh[i] @ vh[lo:hi].T
+            ref["o"].append(p @ vh[lo:hi])
+            ref["dq"].append(scale * ((p * (dp - delta_r[i])) @ kh[lo:hi]))
+            got["o"].append(o[0, i, cs].float())
+            got["dq"].append(dq[0, i, cs].float())
+        # sampled key rows: dK, dV over all allowed queries
+        for j in krows.tolist():
+            f = j // tpf
+            q0, q1 = f * tpf, (L if window is None else min(L, (f + window) * tpf))
+            qi = torch.arange(q0, q1, device=DEV)
+            ok = allowed(qi, torch.tensor([j], device=DEV))[:, 0]
+            s = (qh[q0:q1] @ kh[j]) * scale
+            p = torch.where(ok, torch.exp(s - lse_r[q0:q1]), torch.zeros_like(s))
+            dp = doh[q0:q1] @ vh[j]
+            ref["dv"].append(p @ doh[q0:q1])
+            ref["dk"].append(scale * ((p * (dp - delta_r[q0:q1])) @ qh[q0:q1]))
+            got["dv"].append(dv[0, j, cs].float())
+            got["dk"].append(dk[0, j, cs].float())
+    for n in ("o", "dq", "dk", "dv"):
+        assert rel(torch.stack(got[n]), torch.stack(ref[n])) < 1e-2, n
+
+
 def test_flow_noise_mse():
     k = K()
     B, N, C, h = 2, 3, 32, 8
@@ -330,20 +429,50 @@ def test_colsum(R, N):
 
 @pytest.mark.parametrize("shape", [(256, 768), (768, 256), (128, 128)])
 def test_newton_schulz_matches_oracle(shape):
+    """owlk_newton_schulz_bf16 (one C entry, reference rounding order: the A GEMM also emits
+    bf16(c A), B = bf16(b A) + bf16(cA @ A)) against the reference's own output (ops.pt ns.*.y,
+    generated by the reference's zeropower_via_newtonschulz5) and the oracle: within 2 bf16 ulp of
+    1.0 (max-abs 2^-7).  What remains is the GEMMs' fp32 accumulation order (MFMA vs
+    the CPU's), which flips single bf16 roundings that five chaotic iterations then amplify: rel-L2
+    measured 1.0-1.5 % after 5 steps (2.7 % with the scalar applied after the product, round 1),
+    and after 1-2 steps it stays at the rounding level (test_newton_schulz_steps_vs_oracle)."""
     from conftest import golden
     from owl_wms.muon import newton_schulz_bf16
     ops = golden("ops.pt")
     g = ops[f"ns.{shape[0]}x{shape[1]}.g"]
     y = newton_schulz_bf16(g.to(DEV)[None])[0].float().cpu()
-    # (1) kernel parity: the oracle evaluated in the kernel's rounding order (AXPBY epilogue)
-    mine = R.newton_schulz5(g, order="epilogue").float()
-    assert rel(y, mine) < 2e-2  # fp32 MFMA vs CPU accumulation order, amplified by 5 bf16 NS steps
-    # (2) vs the reference's own output: bf16 NS is chaotic in rounding order (the oracle's two
-    #     orders differ by ~2.7% rel-L2 on these inputs), so 4% and the same singular spectrum
     ref = ops[f"ns.{shape[0]}x{shape[1]}.y"].float()
-    assert rel(y, ref) < 4e-2
-    sv, sr = torch.linalg.svdvals(y), torch.linalg.svdvals(ref)
-    assert (sv - sr).abs().max() < 0.05
+    mine = R.newton_schulz5(g).float()
+    for r in (ref, mine):
+        assert (y - r).abs().max().item() <= 2 ** -7
+        assert rel(y, r) < 2e-2
+
+
+@pytest.mark.parametrize("steps,tol", [(1, 4e-3), (2, 6e-3)])
+@pytest.mark.parametrize("shape", [(256, 768), (768, 256), (128, 128)])
+def test_newton_schulz_steps_vs_oracle(shape, steps, tol):
+    """Before the iteration's chaos amplifies it, the library NS equals the oracle (pinned exactly to
+    the reference's eager body) at the bf16 rounding level: same rounding order, so only fp32
+    accumulation order differs."""
+    from conftest import golden
+    g = golden("ops.pt")[f"ns.{shape[0]}x{shape[1]}.g"]
+    y = K().newton_schulz(g.to(DEV)[None], steps)[0].float().cpu()
+    r = R.newton_schulz5(g, steps).float()
+    assert rel(y, r) < tol, rel(y, r)
+
+
+@pytest.mark.parametrize("count,shape", [(3, (256, 768)), (2, (768, 256)), (16, (64, 128))])
+def test_ns_iterate_equals_library_entry(count, shape):
+    """Muon's in-step NS (normalise -> owlk_ns_iterate on a shape batch) and owlk_newton_schulz_bf16
+    run the same kernels: bit-identical updates."""
+    k = K()
+    r, c = shape
+    g = torch.randn(count, r, c, generator=torch.Generator().manual_seed(90)).to(DEV)
+    whole = k.newton_schulz(g)
+    tr = r > c
+    x = k.ns_iterate(k.ns_normalize(g, tr), 5)
+    x = x.transpose(1, 2) if tr else x
+    assert torch.equal(x, whole)
 
 
 @pytest.mark.parametrize("M,N,K_", [(128, 1536, 16384), (1536, 1536, 20480), (4608, 256, 12288),
@@ -431,12 +560,13 @@ def test_layernorm_fwd_bwd(T, d):
 @pytest.mark.parametrize("shape", [(256, 2), (3, 40), (12, 13)])
 def test_newton_schulz_padded_shapes(shape):
     """Shapes whose dims are not multiples of 8 (mmdit_v2 puts control_embed.mouse.angle_proj
-    [256, 2] under Muon) are zero-padded: same result as the oracle NS in the kernel's order."""
+    [256, 2] under Muon) are zero-padded inside owlk_newton_schulz_bf16: same result as the oracle
+    NS (reference rounding order)."""
     from owl_wms.muon import newton_schulz_bf16
     g = torch.randn(*shape, generator=torch.Generator().manual_seed(80))
     y = newton_schulz_bf16(g[None].to(DEV))[0]
-    ref = R.newton_schulz5(g, 5, order="epilogue")
-    assert y.shape == shape and rel(y, ref) < 2e-2
+    ref = R.newton_schulz5(g, 5)
+    assert y.shape == shape and rel(y, ref) < 1e-2 and (y.float().cpu() - ref.float()).abs().max() <= 2 ** -7
 
 
 def test_single_document_cache():
@@ -477,7 +607,7 @@ def test_muon_momentum_fused(count, shape, misalign, nesterov):
     bufs = [torch.randn(shape, generator=gen).to(DEV) * 0.1 for _ in range(count)]
     exp = [_torch_momentum(g, b, 0.95, nesterov) for g, b in zip(grads, bufs)]
     out = torch.empty(count, n, device=DEV)
-    sumsq = torch.zeros(count, device=DEV)
+    sumsq = torch.full((count, K().NORM_PARTS), float("nan"), device=DEV)  # fully written by the pass
     g_before = [g.clone() for g in grads]
     K().muon_momentum(grads, bufs, 0.95, nesterov, out, sumsq)
     torch.cuda.synchronize()
@@ -485,7 +615,7 @@ def test_muon_momentum_fused(count, shape, misalign, nesterov):
         torch.testing.assert_close(bufs[i], b, rtol=2e-7, atol=1e-7)
         torch.testing.assert_close(out[i].view(shape), gp, rtol=2e-7, atol=1e-7)
         ss = gp.bfloat16().float().pow(2).sum()
-        assert abs(sumsq[i].item() / ss.item() - 1) < 1e-5
+        assert abs(sumsq[i].sum().item() / ss.item() - 1) < 1e-5
         assert torch.equal(grads[i], g_before[i])  # written to the stack, not into p.grad
 
 
@@ -623,9 +753,10 @@ def test_attention_packed_runs_match_general_doc_path(case, D):
 
 
 def test_muon_multirank_path_on_gpu(monkeypatch):
-    """The world_size > 1 branch of Muon.step (round-robin NS + all_gather, muon.py:86-115) on the
-    HIP passes, in one process: the gather is emulated so that this rank's update lands in its slot,
-    and the parameters this rank owns must equal a single-rank step of the same parameters."""
+    """The world_size > 1 branch of Muon.step (round-robin NS + one async all_gather per group,
+    muon.py:86-115) on the HIP passes, in one process: the gather is emulated so that every slot gets
+    this rank's updates, and the parameters this rank owns must equal a single-rank step of the same
+    parameters."""
     import owl_wms.muon as mu
     gen = torch.Generator().manual_seed(31)
     shapes = [(96, 64), (96, 64), (96, 64)]
@@ -639,10 +770,15 @@ def test_muon_multirank_path_on_gpu(monkeypatch):
         mu.Muon(ps, lr=1e-2, momentum=0.95, rank=rank, world_size=ws).step()
         return ps
 
-    def fake_gather(out, inp):  # slot `rank` gets this rank's update, the other slot a copy of it
-        out.copy_(inp.expand_as(out))
+    class Done:
+        def wait(self):
+            pass
 
-    monkeypatch.setattr(mu, "_all_gather", fake_gather)
+    def fake_gather(out, inp):  # slot `rank` gets this rank's updates, the other slot a copy of them
+        out.view(2, -1).copy_(inp.view(1, -1).expand(2, -1))
+        return Done()
+
+    monkeypatch.setattr(mu, "_all_gather_async", fake_gather)
     single = run(1, 0)
     multi = run(2, 0)  # rank 0 of 2 owns params 0 and 2 (chunks [0, 1], [2])
     for i in (0, 2):
@@ -650,25 +786,32 @@ def test_muon_multirank_path_on_gpu(monkeypatch):
 
 
 def test_ema_fused_matches_foreach_lerp():
-    """EMA.update on owlk_ema (one multi-tensor pass) vs torch._foreach_lerp_ (the previous / eager
-    form): 20 tensors incl. odd sizes (scalar path) over 3 updates, within 1e-6 of each tensor's scale."""
+    """EMA.update on owlk_ema (one multi-tensor pass) vs torch._foreach_lerp_ (the eager form of
+    ema_pytorch's update): 20 tensors incl. odd sizes (scalar path) over 5 updates, within 1e-6 of
+    each tensor's scale.  Schedule (ema_pytorch, update_after_step 0): update 0 copies; update 1
+    copies again (sets initted) and lerps at decay 1 - 2^(-2/3) onto equal values; update t >= 2
+    lerps at decay min(0.999, 1 - (1 + t)^(-2/3))."""
     from owl_wms.utils.grad_reducer import EMA
     gen = torch.Generator().manual_seed(41)
     shapes = [(3072, 1536), (1536,), (7,), (128, 11)] + [(64, 64)] * 16
     model = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(s, generator=gen).to(DEV)) for s in shapes])
     ema = EMA(model, beta=0.999)
     ref = None
-    for t in range(4):
+    for t in range(5):
         with torch.no_grad():
             for p in model:
                 p.add_(torch.randn(p.shape, generator=gen).to(DEV) * 0.1)
-        if t == 0:
-            ema.update()
-            ref = [s.clone() for s in ema.shadow]
-            continue
-        decay = min(0.999, 1 - (1 + t - 1) ** (-2 / 3)) if t > 1 else 0.0
-        torch._foreach_lerp_(ref, [p.detach() for p in model], 1.0 - decay)
         ema.update()
+        if t <= 1:
+            assert ema.initted == (t == 1)
+            ref = [p.detach().clone() for p in model]
+        else:
+            decay = min(0.999, 1 - (1 + t) ** (-2 / 3))
+            assert abs(ema.get_current_decay() - decay) < 1e-12
+            torch._foreach_lerp_(ref, [p.detach() for p in model], 1.0 - decay)
     torch.cuda.synchronize()
     for a, b in zip(ema.shadow, ref):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6 * b.abs().max().item())
+    sd = ema.state_dict()
+    assert int(sd["step"]) == 5 and bool(sd["initted"]) and all("ema_model." + k in sd for k, _ in
+                                                                  model.named_parameters())

@@ -76,13 +76,44 @@ def test_gamerft_loss_pred_grads_vs_reference(mode):
     assert n_full >= 6 or mode == "fp32"
 
 
+def test_gamerft_d128_loss_pred_grads_vs_reference():
+    """Head dim 128 (the dit_v4_5B path: D = 128 attention, qk_rope and MotionRoPE tables, gradient
+    checkpointing with the kept attention output) on a tiny d256 / 2-head GameRFT vs the reference's
+    own fixture (tests/golden/make_golden.py d128); bf16 autocast semantics, SURVEY §8(c)."""
+    from owl_wms.configs import model_config
+    from owl_wms.models.flow import InjectedNoise
+    from owl_wms.models.gamerft import GameRFT
+    G = golden("gamerft_d128.pt")
+    p = "d128.bf16."
+    m = det_init_(GameRFT(model_config(**dict(TINY, d_model=256, gradient_checkpointing=True))),
+                  base_seed=1100).cuda().train()
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == G["d128.schema"]
+    m.noise_source = InjectedNoise({"rand_b": G[p + "in.rand_b"], "ts_raw": G[p + "in.ts_raw"], "z": G[p + "in.z"]})
+    d = m(G[p + "in.x"].cuda(), G[p + "in.mouse"].cuda(), G[p + "in.btn"].cuda(), G[p + "in.doc_id"].cuda(),
+          return_dict=True)
+    d["diffusion_loss"].backward()
+    assert torch.equal(d["cfg_mask"].cpu(), G[p + "cfg_mask"])
+    lref = G[p + "loss"].item()
+    assert abs(d["diffusion_loss"].item() - lref) / lref < 5e-3
+    assert rel(d["pred_video"], G[p + "pred"]) < 2e-2
+    n = 0
+    for i, (k, prm) in enumerate(sorted(m.named_parameters())):
+        st = G[p + "gradstat." + k]
+        assert abs(prm.grad.double().norm().item() - st[3].item()) <= 5e-2 * st[3].item() + 1e-7, k
+        if p + "grad." + k in G:
+            assert rel(prm.grad, G[p + "grad." + k]) < 2e-2, (k, rel(prm.grad, G[p + "grad." + k]))
+            n += 1
+    assert n >= 6
+
+
 def test_muon_step_on_reference_grads_gpu():
     """muon.py:66-84 on libowlk NS, fed the reference's own grads.
 
-    Pinned twice: against the oracle Muon step in the kernel's NS rounding order (tight), and
-    against the reference's update with the bf16-NS rounding-order tolerance (measured 2.7-7%)."""
+    The library NS rounds as the eager reference does, so the update is pinned to both the oracle
+    Muon step and the reference's own update (muon.after.full); NS's five chaotic bf16 iterations
+    amplify the remaining fp32 accumulation-order differences to a few % rel-L2 on this [384, 128]
+    gradient (0.1 in round 1, with the scalar applied after the product)."""
     from oracle.ref_model import muon_step_1rank
-    from oracle import ref_ops as R
     from owl_wms.muon import Muon
     k = "core.transformer.blocks.0.attn.qkv.weight"
     m = _model()
@@ -90,18 +121,13 @@ def test_muon_step_on_reference_grads_gpu():
     p0 = prm.detach().clone()
     prm.grad = GR["gamerft.fp32.grad." + k].cuda().clone()
     Muon([prm], lr=1e-3, momentum=0.95, rank=0, world_size=1).step()
-    # oracle in the epilogue rounding order
     q = torch.nn.Parameter(p0.cpu().clone())
     q.grad = GR["gamerft.fp32.grad." + k].clone()
-    orig = R.newton_schulz5
-    R.newton_schulz5 = lambda G, steps=5: orig(G, steps, order="epilogue")
-    try:
-        muon_step_1rank([q], {}, lr=1e-3, momentum=0.95)
-    finally:
-        R.newton_schulz5 = orig
-    assert rel(prm.detach() - p0, q.detach() - p0.cpu()) < 1e-2
+    muon_step_1rank([q], {}, lr=1e-3, momentum=0.95)
+    r_oracle = rel(prm.detach() - p0, q.detach() - p0.cpu())
     ref = GR["muon.after.full." + k]
-    assert rel(prm.detach() - p0, ref - p0.cpu()) < 0.1
+    r_ref = rel(prm.detach() - p0, ref - p0.cpu())
+    assert r_oracle < 5e-2 and r_ref < 5e-2, (r_oracle, r_ref)
 
 
 def test_combined_optimizer_partition_and_step():
@@ -438,3 +464,118 @@ def test_data_parallel_step_two_ranks_on_gpu():
     assert res[0].keys() == res[1].keys()
     for k in res[0]:
         assert (res[0][k] == res[1][k]).all(), k
+
+
+def _tiny_trainer_cfg(tmp_path, **train_over):
+    import yaml
+    from owl_wms.configs import Config
+    train = {"trainer_id": "rft", "data_id": "synthetic", "data_kwargs": {"window_length": 8},
+             "target_batch_size": 2, "batch_size": 1, "epochs": 1, "opt": "Muon",
+             "opt_kwargs": yaml.safe_load(open(os.path.join(REPO, "configs", "dit_v4.yml")))["train"]["opt_kwargs"],
+             "checkpoint_dir": str(tmp_path / "ckpt"), "save_interval": 2, "sample_interval": 10 ** 9,
+             "vae_scale": 1.0, "seed": 77}
+    train.update(train_over)
+    (tmp_path / "c.yml").write_text(yaml.safe_dump({"model": dict(TINY), "train": train,
+                                                    "wandb": {"project": "p", "run_name": "r"}}))
+    return Config.from_yaml(str(tmp_path / "c.yml"))
+
+
+def _step_keyed_trainer():
+    """RFTTrainer whose synthetic batches are keyed by the global optimizer step (a resumed run
+    restarts its loader, as the reference's does; keying by step gives both runs the same data)."""
+    from owl_wms.data import synthetic_video_batch
+    from owl_wms.trainers.rft_trainer import RFTTrainer
+
+    class T(RFTTrainer):
+        def loader(self):
+            tr = self
+
+            class L:
+                def __iter__(self):
+                    i = 0
+                    while True:
+                        yield synthetic_video_batch(tr.model_cfg, 1, seed=500 + 10 * tr.total_step_counter + i % 2,
+                                                    n_docs=1 + i % 2)
+                        i += 1
+            return L()
+    return T
+
+
+def test_trainer_resume_equals_uninterrupted(tmp_path):
+    """rft_trainer.py:64-121 + base.py:61-72: 2 Muon steps -> save -> a fresh trainer with
+    resume_ckpt (model / EMA keys through the prefix strip, strict load) -> 1 more step gives the
+    same parameters, EMA weights and optimizer state as 3 uninterrupted steps, bit for bit."""
+    T = _step_keyed_trainer()
+    c = _tiny_trainer_cfg(tmp_path)
+    a = T(c.train, c.wandb, c.model, 0, 0, 1)
+    a.max_steps = 3
+    a.train()
+    ck = tmp_path / "ckpt" / "step_2.pt"
+    assert ck.exists()
+    state = torch.load(ck, weights_only=True)
+    assert set(state) == {"model", "ema", "opt", "steps"} and state["steps"] == 2
+    # a reference-style checkpoint: compiled + DDP prefixes on model and EMA keys
+    state["model"] = {"_orig_mod.module." + k: v for k, v in state["model"].items()}
+    state["ema"] = {(k.replace("ema_model.", "ema_model._orig_mod.module.") if k.startswith("ema_model.") else k): v
+                    for k, v in state["ema"].items()}
+    torch.save(state, tmp_path / "ref_style.pt")
+    (tmp_path / "b").mkdir(exist_ok=True)
+    c2 = _tiny_trainer_cfg(tmp_path / "b", resume_ckpt=str(tmp_path / "ref_style.pt"))
+    b = T(c2.train, c2.wandb, c2.model, 0, 0, 1)
+    b.max_steps = 1
+    b.train()
+    assert b.total_step_counter == a.total_step_counter == 3
+    assert b.history[0]["diffusion_loss"] == a.history[2]["diffusion_loss"]
+    for (k, p), (k2, q) in zip(a.model.named_parameters(), b.model.named_parameters()):
+        assert k == k2 and torch.equal(p, q), k
+    for s, t in zip(a.ema.shadow, b.ema.shadow):
+        assert torch.equal(s, t)
+    assert a.ema.step == b.ema.step == 3
+    sa, sb = a.opt.state_dict(), b.opt.state_dict()
+    for part in ("adamw", "muon"):
+        assert sa[part]["param_groups"] == sb[part]["param_groups"]
+        for i, st in sa[part]["state"].items():
+            for kk, v in st.items():
+                assert torch.equal(v, sb[part]["state"][i][kk]), (part, i, kk)
+
+
+def test_trainer_eval_sampler_at_sample_interval(tmp_path):
+    """rft_trainer.py:213, 243-280: the EMA model's sampler runs at step 0 and every
+    sample_interval; latents land in eval_sample_dir as vid.<step>.pt (4 context + 2 generated)."""
+    from owl_wms.trainers import get_trainer_cls
+    c = _tiny_trainer_cfg(tmp_path, sample_interval=2, sampler_id="av_caching", n_samples=1,
+                          sampler_kwargs={"n_steps": 2, "cfg_scale": 1.0, "num_frames": 2, "noise_prev": 0.2,
+                                          "only_return_generated": False},
+                          sample_data_id="cod", sample_data_kwargs={"window_length": 4},
+                          eval_sample_dir=str(tmp_path / "eval"))
+    tr = get_trainer_cls("rft")(c.train, c.wandb, c.model, 0, 0, 1)
+    tr.max_steps = 3
+    tr.train()
+    assert [("eval/frames" in h) for h in tr.history] == [True, False, True]
+    for step in (0, 2):
+        v = torch.load(tmp_path / "eval" / f"vid.{step}.pt", weights_only=True)
+        assert v.shape == (1, 6, 32, 8, 8) and torch.isfinite(v.float()).all()
+
+
+def test_optimizer_step_refreshes_bf16_weights():
+    """The fused optimizer passes write parameters through raw pointers; the version-keyed bf16
+    weight caches must see it: after a Muon + AdamW step the model's forward equals that of a fresh
+    model holding the same weights (bit for bit)."""
+    from owl_wms.muon import init_muon
+    from owl_wms.models.flow import InjectedNoise
+    m, _ = _run("bf16")
+    opt = init_muon(m, rank=0, world_size=1, lr=1e-2, momentum=0.95, adamw_lr=1e-2, adamw_wd=1e-4, adamw_eps=1e-15,
+                    adamw_betas=[0.9, 0.95], adamw_keys=["core.proj_in", "core.proj_out.proj", "core.t_embed",
+                                                         "core.control_embed", "gate", "adaln"])
+    opt.step()
+    fresh = _model()
+    fresh.load_state_dict(m.state_dict())
+    p = "gamerft.bf16."
+    outs = []
+    for mm in (m, fresh):
+        mm.noise_source = InjectedNoise({"rand_b": GR[p + "in.rand_b"], "ts_raw": GR[p + "in.ts_raw"],
+                                         "z": GR[p + "in.z"]})
+        with torch.no_grad():
+            outs.append(mm(GR[p + "in.x"].cuda(), GR[p + "in.mouse"].cuda(), GR[p + "in.btn"].cuda(),
+                           GR[p + "in.doc_id"].cuda(), return_dict=True)["pred_video"])
+    assert torch.equal(outs[0], outs[1])

@@ -215,3 +215,42 @@ def test_mmdit_bf16_autocast_loss_pred_grads():
             assert ((prm.grad.double() - ref.double()).norm() / ref.double().norm()).item() < 1e-2, k
             n += 1
     assert n >= 10
+
+
+# ----------------------------------------------------------------------------- head dim 128 (configs[4])
+D128 = golden("gamerft_d128.pt")
+
+
+def test_motion_rope_tables_d128():
+    """MotionRoPE at head_dim 128 (dit_v4_5B: d 2560 / 20 heads, rope.py:88-152): exact."""
+    big = R.motion_rope_angles(1536, 8, 128)
+    assert list(big.shape) == D128["mrope.5b.shape"]
+    for part, sl in (("head", slice(0, 128)), ("tail", slice(-128, None))):
+        close(big[sl].cos(), D128[f"mrope.5b.cos.{part}"], 0, 0)
+        close(big[sl].sin(), D128[f"mrope.5b.sin.{part}"], 0, 0)
+    a = R.motion_rope_angles(8, 8, 128)
+    close(R.rope_apply(D128["rope128.x"], a.cos(), a.sin()), D128["rope128.y"], 0, 0)
+    assert torch.equal(R.rope_apply(D128["rope128.xb"], a.cos(), a.sin()), D128["rope128.yb"])
+
+
+def test_gamerft_d128_bf16_autocast_loss_pred_grads():
+    """Tiny D = 128 GameRFT (d 256, 2 heads, gradient checkpointing) under bf16 autocast: the oracle
+    reproduces the reference's loss, prediction and gradients."""
+    p = "d128.bf16."
+    model = det_init_(M.GameRFT(tiny_cfg(d_model=256, n_heads=2)), base_seed=1100).train()
+    assert [[k, list(v.shape)] for k, v in model.state_dict().items()] == D128["d128.schema"]
+    noise = {"rand_b": D128[p + "in.rand_b"], "ts_raw": D128[p + "in.ts_raw"], "z": D128[p + "in.z"]}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        loss, pred, hc = model(D128[p + "in.x"], D128[p + "in.mouse"], D128[p + "in.btn"], D128[p + "in.doc_id"],
+                               noise)
+    loss.backward()
+    assert torch.equal(hc, D128[p + "cfg_mask"])
+    assert abs(loss.item() - D128[p + "loss"].item()) <= 1e-4 * D128[p + "loss"].item()
+    close(pred, D128[p + "pred"], 2e-2, 2e-2)
+    n = 0
+    for k, prm in model.named_parameters():
+        if p + "grad." + k in D128:
+            ref = D128[p + "grad." + k]
+            assert ((prm.grad.double() - ref.double()).norm() / ref.double().norm()).item() < 1e-2, k
+            n += 1
+    assert n >= 6
