@@ -59,8 +59,9 @@ def cpu_baseline(steps=3):
 
     from oracle import ref_model as M
     from oracle.params import det_tensor
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = min(ncpu, 16)
+    # every core this process may run on (os.cpu_count(), narrowed to the affinity
+    # mask the box grants); the number of threads actually used is reported as `cores`
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     torch.set_num_threads(cores)
     cfg = SimpleNamespace(model_id="game_rft", sample_size=8, channels=128, n_layers=16, n_heads=24, d_model=1536,
                           tokens_per_frame=64, n_buttons=11, cfg_prob=0.1, n_frames=16, causal=True, uncond=False,
@@ -88,6 +89,76 @@ def cpu_baseline(steps=3):
                       f"sequence than the GPU workload"}
 
 
+def live_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` on this box, this run (MI355X_MICROARCH.md §HBM): two
+    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) over one fwd+bwd
+    micro-step of the same model (bench.py --microsteps 1), restricted to the kernel; FETCH_SIZE
+    doubled (gfx950 counts half the bytes of 16-B/lane streaming reads), both in KiB.  Child
+    processes, after the timed region; None if rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import glob
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    sym = {"attn_bwd_dkdv": "attn_bwd_dkdv_k", "attn_bwd_dq": "attn_bwd_dq_k", "attn_fwd": "attn_fwd"}.get(kernel)
+    if sym is None:
+        return None
+    out = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="owlk_pmc_", dir="/tmp")
+        cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", sym, "-f", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--microsteps", "1", "--config", args.config,
+               "--docs", str(args.docs)]
+        if args.frames:
+            cmd += ["--frames", str(args.frames)]
+        try:
+            subprocess.run(cmd, cwd="/tmp", env=env, timeout=240, check=True, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+        except (subprocess.SubprocessError, OSError) as e:
+            log(f"[bench] PMC pass {ctr} failed: {e}")
+            return None
+        vals = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if re.search(sym, r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
+                    vals.append(float(r["Counter_Value"]) * 1024)
+        shutil.rmtree(d, ignore_errors=True)
+        if not vals:
+            return None
+        out[ctr] = (2.0 if ctr == "FETCH_SIZE" else 1.0) * sum(vals) / len(vals)
+        out["launches"] = len(vals)
+    return {"bytes": out["FETCH_SIZE"] + out["WRITE_SIZE"], "fetch": out["FETCH_SIZE"], "write": out["WRITE_SIZE"],
+            "launches": out["launches"]}
+
+
+def microsteps(args):
+    """--microsteps K: K fwd+bwd micro-steps of the configured model and nothing else (the PMC passes
+    of live_traffic run this under rocprofv3)."""
+    from owl_wms.configs import Config
+    from owl_wms.data import synthetic_video_batch
+    from owl_wms.models import get_model_cls
+    cfg = Config.from_yaml(os.path.join(REPO, args.config))
+    mc = cfg.model
+    if args.frames:
+        mc.n_frames = args.frames
+    torch.manual_seed(0)
+    model = get_model_cls(mc.model_id)(mc).cuda().train()
+    b = [t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234, n_docs=args.docs)]
+    for _ in range(args.microsteps):
+        if mc.model_id == "game_rft_audio":
+            au = torch.randn(1, mc.n_frames, mc.audio_channels, device="cuda").to(torch.bfloat16)
+            loss = model(b[0] / cfg.train.vae_scale, au, b[1], b[2])[0]
+        else:
+            loss = model(b[0] / cfg.train.vae_scale, b[1], b[2], b[3])
+        loss.backward()
+        model.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,7 +174,11 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--config", default="configs/dit_v4.yml",
                     help="model config; the headline metric is dit_v4 (others, e.g. dit_v4_5B, report their own line)")
+    ap.add_argument("--microsteps", type=int, default=0, help="(internal) run K fwd+bwd micro-steps and exit")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the live PMC traffic passes")
     args = ap.parse_args()
+    if args.microsteps:
+        return microsteps(args)
 
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
         os.environ.get("LOCAL_RANK", 0))
@@ -219,16 +294,19 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
                 "launches_per_microstep": n, "avg_launch_ms": round(ms / n, 4),
                 "share_of_microstep_kernel_time": round(ms / tot_ms, 3)}
-        # HBM bytes per launch of the same kernel on this same command, from the committed PMC passes
-        # (tools/pmc_traffic.sh -> tools/traffic_summary.py -> profiles/<round>_traffic.json)
-        import glob
-        tf = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
-        if tf:
-            rec = json.load(open(tf[-1])).get(dom)
-            if rec:
-                roof["traffic"] = round(rec["traffic_bytes_per_launch"])
-                roof["traffic_unit"] = "bytes/launch (HBM, PMC)"
-                roof["traffic_source"] = os.path.relpath(tf[-1], REPO)
+        # HBM bytes per launch of the same kernel, measured now on this box (PMC passes in child
+        # processes over one micro-step of the same model)
+        if rank == 0 and world == 1 and not args.no_traffic:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            tr = live_traffic(dom, args)
+            if tr:
+                roof["traffic"] = round(tr["bytes"])
+                roof["traffic_unit"] = "bytes/launch (HBM, PMC, this run)"
+                roof["traffic_detail"] = {"fetch": round(tr["fetch"]), "write": round(tr["write"]),
+                                          "launches": tr["launches"],
+                                          "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
+                                                    "one micro-step; FETCH_SIZE x2 (gfx950)"}
         if rank == 0:
             log("[bench] per-kernel time in one micro-step (ms):")
             for k, (n, ms_, fl_) in kernels[:40]:

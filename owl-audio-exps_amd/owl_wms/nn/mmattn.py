@@ -15,7 +15,12 @@ and the mirrored backward.  The modulation is shared by every layer (DiT-Air, mm
 
 The reference module imports a missing ``create_causal_block_mask``; its
 mask is reconstructed as get_block_mask(n, tpf, window, no docs, q_offset, causal) -- a
-FrameMask here.  Decode-time KV caching through MMDiT is not implemented (kv_cache must be None).
+FrameMask here.
+
+KV cache (mmattn.py:46-72, decode / sampling, no grad): the new joint frame(s) are rotated at
+offset = the layer's cached length, [cache | new] K/V are read in place (SingleKVCache.extend),
+the cache is committed when updates are enabled, and the attention keeps the frame mask with
+q_offset = the cached length (the reference's create_causal_block_mask(n_cached_tokens=offset)).
 """
 import torch
 import torch.nn.functional as F
@@ -162,7 +167,8 @@ class MMDiTBlock(nn.Module):
 
     def forward(self, x0, x1, cond0, cond1, block_mask=None, kv_cache=None):
         if kv_cache is not None:
-            raise NotImplementedError("MMDiT decode-time KV caching is not implemented on libowlk")
+            with torch.no_grad():
+                return self._forward_cached(x0, x1, cond0, cond1, block_mask, kv_cache)
         cfg, a = self.config, self.attn
         H = cfg.n_heads
         n0 = cfg.sample_size ** 2
@@ -178,6 +184,54 @@ class MMDiTBlock(nn.Module):
         return MMDiTBlockFn.apply(x0.to(BF16).contiguous(), x1.to(BF16).contiguous(), cond0, cond1, geo, *ws)
 
 
+    def _forward_cached(self, x0, x1, cond0, cond1, block_mask, kv_cache):
+        """MMDiTBlock.forward (mmattn.py:98-114) with MMAttn's cache path (mmattn.py:46-72)."""
+        cfg, a = self.config, self.attn
+        d, H = cfg.d_model, cfg.n_heads
+        D = d // H
+        n0, n1 = cfg.sample_size ** 2, 1
+        B, T0, _ = x0.shape
+        nf = T0 // n0
+        T = nf * (n0 + n1)
+        ns = (n0, n1)
+        xs = (x0.reshape(-1, d).to(BF16).contiguous(), x1.reshape(-1, d).to(BF16).contiguous())
+        ms = (cond0.reshape(B * nf, 6 * d), cond1.reshape(B * nf, 6 * d))
+        qkv = []
+        for s in range(2):
+            h, _ = K.adaln_fwd(xs[s], ms[s][:, :d], ms[s][:, d:2 * d], ns[s])
+            qkv.append(K.gemm(h, bf16_weight(a.qkv_projs[s].weight), bias=a.qkv_projs[s].bias))
+        qkvj = K.frame_interleave(qkv[0], qkv[1], n0, n1)
+        del qkv
+        li = a.layer_idx
+        offset = kv_cache.length_at(li)
+        qkr, _ = K.qk_rope_fwd(qkvj, H, D, a.rope.cos, a.rope.sin, offset, T)
+        q = qkr.view(B, T, 2 * d)[:, :, :d]
+        k = qkr.view(B, T, 2 * d)[:, :, d:]
+        v = qkvj.view(B, T, 3 * d)[:, :, 2 * d:]
+        if offset > 0:
+            if kv_cache.noise_caches == 0.0 and hasattr(kv_cache, "extend"):
+                k, v = kv_cache.extend(li, k, v)
+            else:
+                old_k, old_v = kv_cache.get(li)
+                k, v = torch.cat([old_k, k], dim=1), torch.cat([old_v, v], dim=1)
+        if kv_cache.should_update:
+            kv_cache.update(k, v, li)
+        mask = block_mask if block_mask is not None else K.FrameMask(1, None, False, 0, None)
+        o, _ = K.attn_fwd(q, k, v, H, D, mask, score_bound=K.qk_norm_bound(D))
+        os_ = K.frame_split(o.view(B * T, d), n0, n1)
+        outs = []
+        for s in range(2):
+            x1s = K.gemm(os_[s], bf16_weight(a.out_projs[s].weight), bias=a.out_projs[s].bias, epi=K.EPI_GATE_RESID,
+                         gate=ms[s][:, 2 * d:3 * d], tpf=ns[s], resid=xs[s])
+            h2, _ = K.adaln_fwd(x1s, ms[s][:, 3 * d:4 * d], ms[s][:, 4 * d:5 * d], ns[s])
+            m = self.mlps[s]
+            a_pre = torch.empty(x1s.shape[0], m.fc1.weight.shape[0], device=x0.device, dtype=BF16)
+            act = K.gemm(h2, bf16_weight(m.fc1.weight), bias=m.fc1.bias, epi=K.EPI_SILU, aux=a_pre)
+            outs.append(K.gemm(act, bf16_weight(m.fc2.weight), bias=m.fc2.bias, epi=K.EPI_GATE_RESID,
+                               gate=ms[s][:, 5 * d:], tpf=ns[s], resid=x1s))
+        return outs[0].view(B, T0, d), outs[1].view(B, nf, d)
+
+
 class MMDIT(nn.Module):
     def __init__(self, config):
         super().__init__()
@@ -189,9 +243,11 @@ class MMDIT(nn.Module):
         self.cond_proj = nn.Sequential(nn.SiLU(), nn.Linear(config.d_model, config.d_model * 2 * 2 * 3))
 
     def get_block_mask(self, x0, x1, kv_cache, window_len):
+        """mmattn.py:132-143: causal frame mask over [cache | new] (q_offset = cached tokens)."""
         if not self.config.causal:
             return K.FrameMask(self.config.tokens_per_frame, None, False, 0, None)
-        return K.FrameMask(self.config.tokens_per_frame, window_len, True, 0, None)
+        offset = kv_cache.length_at(0) if kv_cache is not None else 0
+        return K.FrameMask(self.config.tokens_per_frame, window_len, True, offset, None)
 
     def forward(self, x0, x1, cond, kv_cache=None):
         local_mask = self.get_block_mask(x0, x1, kv_cache, self.config.local_window)

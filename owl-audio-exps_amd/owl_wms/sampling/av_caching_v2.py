@@ -5,6 +5,13 @@ N(0, 1) at t = 1, takes ``n_steps`` Euler steps x -= dt_i v (optional CFG with n
 is re-noised (zlerp) and appended to the cache.  In decode mode the attention is unmasked over
 [cache | new frame]; local layers keep the last local_window frames.  Noise is drawn with
 torch.randn_like in the reference's order (context zlerp, then per frame: x0, then zlerp).
+
+CFG (cfg_scale != 1): the reference runs the conditional and the null-control forward one after
+the other over the same cache (av_caching_v2.py:98-118).  Here both run as ONE forward of batch
+2B -- rows [cond | uncond] -- so each Euler step streams the weights once at twice the rows (a
+decode step is weight-streaming bound).  The cache holds the context twice (both halves cached
+from the conditioned passes, exactly what the reference's single cache holds), so every row sees
+the keys the reference's forward sees.
 """
 import torch
 
@@ -29,11 +36,15 @@ class AVCachingSamplerV2:
         return x * (1.0 - alpha) + z * alpha
 
     def _euler_step(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
-        """av_caching_v2.py:96-110: one Euler step with optional CFG."""
-        pred_v = model(x, t, mouse, btn, kv_cache=kv_cache)
+        """av_caching_v2.py:96-110: one Euler step with optional CFG (cond | uncond as one 2B batch)."""
         if self.cfg_scale != 1.0:
-            pred_u = model(x, t, null_mouse, null_btn, kv_cache=kv_cache)
+            B = x.shape[0]
+            pred = model(torch.cat([x, x]), torch.cat([t, t]), torch.cat([mouse, null_mouse]),
+                         torch.cat([btn, null_btn]), kv_cache=kv_cache)
+            pred_v, pred_u = pred[:B], pred[B:]
             pred_v = pred_u + self.cfg_scale * (pred_v - pred_u)
+        else:
+            pred_v = model(x, t, mouse, btn, kv_cache=kv_cache)
         return x - dt * pred_v, t - dt
 
     def _euler_graphed(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
@@ -72,9 +83,13 @@ class AVCachingSamplerV2:
         if self.custom_schedule is None:
             dt = get_sd3_euler(self.n_steps).to(device=x.device, dtype=x.dtype)
         else:
-            dt = get_deltas(self.custom_schedule)
+            # Python floats in the reference: fp32 device scalars (same opmath; a captured graph
+            # reads them from device memory)
+            dt = torch.tensor(get_deltas(list(self.custom_schedule)), device=x.device, dtype=torch.float32)
+        cfg = self.cfg_scale != 1.0
+        rep = (lambda *ts: [torch.cat([a, a]) for a in ts]) if cfg else (lambda *ts: list(ts))
         kv_cache = KVCache(model.config)
-        kv_cache.reset(batch_size)
+        kv_cache.reset(2 * batch_size if cfg else batch_size)
 
         latents = [x.clone()]
         prev_x = x
@@ -82,7 +97,7 @@ class AVCachingSamplerV2:
         prev_x_noisy = self.zlerp(prev_x, self.noise_prev)
         prev_t = prev_x.new_full((batch_size, prev_x.size(1)), self.noise_prev)
         kv_cache.enable_cache_updates()
-        model(prev_x_noisy, prev_t, prev_mouse, prev_btn, kv_cache=kv_cache)
+        model(*rep(prev_x_noisy, prev_t, prev_mouse, prev_btn), kv_cache=kv_cache)
         kv_cache.disable_cache_updates()
 
         num_frames = min(self.num_frames, mouse.size(1) - init_len)
@@ -104,7 +119,7 @@ class AVCachingSamplerV2:
                 curr_x_noisy = self.zlerp(curr_x, self.noise_prev)
                 curr_t_noisy = torch.ones_like(curr_t) * self.noise_prev
                 kv_cache.enable_cache_updates()
-                model(curr_x_noisy, curr_t_noisy, curr_mouse, curr_btn, kv_cache=kv_cache)
+                model(*rep(curr_x_noisy, curr_t_noisy, curr_mouse, curr_btn), kv_cache=kv_cache)
                 kv_cache.disable_cache_updates()
                 if self.max_window is not None and len(latents) > self.max_window:
                     kv_cache.truncate(1, front=False)

@@ -240,6 +240,35 @@ def test_mmdit_loss_pred_grads_vs_reference():
     assert n >= 10
 
 
+@pytest.mark.parametrize("n_ctx", [5, 3])
+def test_mmdit_kv_cache_decode_matches_full_forward(n_ctx):
+    """MMDiT cache path (mmattn.py:46-72): the context frames cached, then the next joint frame(s)
+    decoded against the cache (RoPE at the cached offset, frame mask with q_offset = cached tokens,
+    local window 2 / global window 4 frames) == the same frames of the full masked forward."""
+    from owl_wms.configs import model_config
+    from owl_wms.models.gamerft_audio import GameRFTAudio
+    from owl_wms.nn.kv_cache import KVCache
+    m = det_init_(GameRFTAudio(model_config(**MMCFG)), base_seed=5000).cuda().eval()
+    core = m.core
+    B, n = 2, 6
+    x = det_tensor((B, n, 32, 8, 8), 910).cuda().bfloat16()
+    au = det_tensor((B, n, 16), 911).cuda().bfloat16()
+    t = torch.sigmoid(det_tensor((B, n), 912)).cuda().bfloat16()
+    mouse = det_tensor((B, n, 2), 913).cuda().bfloat16()
+    btn = (det_tensor((B, n, 11), 914) > 0).cuda().bfloat16()
+    with torch.no_grad():
+        fv, fa = core(x, au, t, mouse, btn)
+        cache = KVCache(core.config)
+        cache.reset(B)
+        cache.enable_cache_updates()
+        cv, ca = core(x[:, :n_ctx], au[:, :n_ctx], t[:, :n_ctx], mouse[:, :n_ctx], btn[:, :n_ctx], kv_cache=cache)
+        cache.disable_cache_updates()
+        assert cache.length_at(0) == n_ctx * 65
+        lv, la = core(x[:, n_ctx:], au[:, n_ctx:], t[:, n_ctx:], mouse[:, n_ctx:], btn[:, n_ctx:], kv_cache=cache)
+    assert rel(cv, fv[:, :n_ctx]) < 1e-5 and rel(ca, fa[:, :n_ctx]) < 1e-5  # the context pass is the masked forward
+    assert rel(lv, fv[:, n_ctx:]) < 2e-2 and rel(la, fa[:, n_ctx:]) < 2e-2
+
+
 class _Draws:
     """Replay torch.randn / randn_like draws (reference order) on the draw's device/dtype."""
 
@@ -396,10 +425,11 @@ def test_trainer_reads_packed_table(tmp_path):
     assert all(torch.isfinite(torch.tensor(h["diffusion_loss"])) for h in tr.history)
 
 
-@pytest.mark.parametrize("n_steps,cfg", [(4, 1.3), (3, 1.0)])
-def test_graphed_decode_equals_eager(n_steps, cfg):
+@pytest.mark.parametrize("n_steps,cfg,custom", [(4, 1.3, None), (3, 1.0, None), (3, 1.3, [1.0, 0.7, 0.3])])
+def test_graphed_decode_equals_eager(n_steps, cfg, custom):
     """compile_on_decode: the per-frame Euler steps replayed from a HIP graph give the same sampled
-    latents as the eager loop, bit for bit (same kernels, same buffers' contents, same order)."""
+    latents as the eager loop, bit for bit (same kernels, same buffers' contents, same order);
+    also with a custom schedule (its deltas live in device memory the graph reads)."""
     from owl_wms.sampling import get_sampler_cls
     m = _model().eval()
     g = torch.Generator().manual_seed(5)
@@ -409,7 +439,8 @@ def test_graphed_decode_equals_eager(n_steps, cfg):
     outs = []
     for graphed in (False, True):
         torch.manual_seed(123)
-        s = get_sampler_cls("av_caching")(n_steps=n_steps, cfg_scale=cfg, num_frames=4, noise_prev=0.2)
+        s = get_sampler_cls("av_caching")(n_steps=n_steps, cfg_scale=cfg, num_frames=4, noise_prev=0.2,
+                                          custom_schedule=custom)
         outs.append(s(m.core, x, mouse, btn, compile_on_decode=graphed))
     assert outs[0].shape == (2, 8, 32, 8, 8)
     assert torch.equal(outs[0], outs[1])
