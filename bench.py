@@ -53,15 +53,28 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def usable_cpus():
+    """BASELINE.md §4's os.cpu_count(), narrowed to the CPUs this process may actually use: the
+    affinity mask and the cgroup CPU quota (cpu.max).  On the GPU boxes os.cpu_count() reports the
+    whole machine while the process is granted a 16-CPU share; threads past the quota only
+    contend (a step with one thread per machine core did not finish in 3 minutes)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(steps=3):
     """fp32 CPU oracle (oracle/ref_model.py) at dit_v4 width/depth, 16 frames = 1,024 tokens."""
     from types import SimpleNamespace
 
     from oracle import ref_model as M
     from oracle.params import det_tensor
-    # every core this process may run on (BASELINE.md §4: os.cpu_count(), narrowed to the affinity
-    # mask the box grants); the number of threads actually used is reported as `cores`
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = usable_cpus()
     torch.set_num_threads(cores)
     cfg = SimpleNamespace(model_id="game_rft", sample_size=8, channels=128, n_layers=16, n_heads=24, d_model=1536,
                           tokens_per_frame=64, n_buttons=11, cfg_prob=0.1, n_frames=16, causal=True, uncond=False,
@@ -89,12 +102,16 @@ def cpu_baseline(steps=3):
                       f"sequence than the GPU workload"}
 
 
-def live_traffic(kernel, args):
-    """HBM bytes per launch of `kernel` on this box, this run (MI355X_MICROARCH.md §HBM): two
-    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) over one fwd+bwd
-    micro-step of the same model (bench.py --microsteps 1), restricted to the kernel; FETCH_SIZE
-    doubled (gfx950 counts half the bytes of 16-B/lane streaming reads), both in KiB.  Child
-    processes, after the timed region; None if rocprofv3 is unavailable or a pass fails."""
+PMC_KERNELS = {"attn_bwd_dkdv": "attn_bwd_dkdv_k", "attn_bwd_dq": "attn_bwd_dq_k", "attn_fwd": "attn_fwd"}
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of the attention kernels on this box, this run (MI355X_MICROARCH.md
+    §HBM): two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) over one
+    fwd+bwd micro-step of the same model (bench.py --microsteps 1), restricted to the kernels;
+    FETCH_SIZE doubled (gfx950 counts half the bytes of 16-B/lane streaming reads), both in KiB.
+    Run as child processes BEFORE this process touches the GPU (a pass next to a live parent
+    context was seen to hang).  -> {kernel: {...}} or {} if rocprofv3 is unavailable / a pass fails."""
     import csv
     import glob
     import re
@@ -102,42 +119,43 @@ def live_traffic(kernel, args):
     import subprocess
     import tempfile
     if not shutil.which("rocprofv3"):
-        return None
-    sym = {"attn_bwd_dkdv": "attn_bwd_dkdv_k", "attn_bwd_dq": "attn_bwd_dq_k", "attn_fwd": "attn_fwd"}.get(kernel)
-    if sym is None:
-        return None
-    out = {}
+        return {}
+    regex = "|".join(PMC_KERNELS.values())
+    vals = {}
     env = dict(os.environ, TMPDIR="/tmp")
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="owlk_pmc_", dir="/tmp")
-        cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", sym, "-f", "csv", "-d", d, "-o", "run", "--",
+        cmd = ["rocprofv3", "--pmc", ctr, "--kernel-include-regex", regex, "-f", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--microsteps", "1", "--config", args.config,
                "--docs", str(args.docs)]
         if args.frames:
             cmd += ["--frames", str(args.frames)]
-        try:
-            subprocess.run(cmd, cwd="/tmp", env=env, timeout=240, check=True, stdout=subprocess.DEVNULL,
-                           stderr=subprocess.DEVNULL)
+        log(f"[bench] PMC pass {ctr} (rocprofv3, one micro-step) ...")
+        try:  # the child's progress goes to this stderr (a silent minute reads as a hang)
+            subprocess.run(cmd, cwd="/tmp", env=env, timeout=240, check=True, stdout=sys.stderr, stderr=sys.stderr)
         except (subprocess.SubprocessError, OSError) as e:
             log(f"[bench] PMC pass {ctr} failed: {e}")
-            return None
-        vals = []
+            return {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if re.search(sym, r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
-                    vals.append(float(r["Counter_Value"]) * 1024)
+                if r.get("Counter_Name") != ctr:
+                    continue
+                for k, sym in PMC_KERNELS.items():
+                    if re.search(sym, r.get("Kernel_Name", "")):
+                        vals.setdefault(k, {}).setdefault(ctr, []).append(float(r["Counter_Value"]) * 1024)
         shutil.rmtree(d, ignore_errors=True)
-        if not vals:
-            return None
-        out[ctr] = (2.0 if ctr == "FETCH_SIZE" else 1.0) * sum(vals) / len(vals)
-        out["launches"] = len(vals)
-    return {"bytes": out["FETCH_SIZE"] + out["WRITE_SIZE"], "fetch": out["FETCH_SIZE"], "write": out["WRITE_SIZE"],
-            "launches": out["launches"]}
+    out = {}
+    for k, v in vals.items():
+        if len(v) == 2:
+            fetch = 2.0 * sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
+            write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"])
+            out[k] = {"bytes": fetch + write, "fetch": fetch, "write": write, "launches": len(v["FETCH_SIZE"])}
+    return out
 
 
 def microsteps(args):
     """--microsteps K: K fwd+bwd micro-steps of the configured model and nothing else (the PMC passes
-    of live_traffic run this under rocprofv3)."""
+    of pmc_traffic run this under rocprofv3)."""
     from owl_wms.configs import Config
     from owl_wms.data import synthetic_video_batch
     from owl_wms.models import get_model_cls
@@ -146,9 +164,11 @@ def microsteps(args):
     if args.frames:
         mc.n_frames = args.frames
     torch.manual_seed(0)
+    log("[microsteps] building the model")
     model = get_model_cls(mc.model_id)(mc).cuda().train()
     b = [t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234, n_docs=args.docs)]
-    for _ in range(args.microsteps):
+    for i in range(args.microsteps):
+        log(f"[microsteps] micro-step {i}")
         if mc.model_id == "game_rft_audio":
             au = torch.randn(1, mc.n_frames, mc.audio_channels, device="cuda").to(torch.bfloat16)
             loss = model(b[0] / cfg.train.vae_scale, au, b[1], b[2])[0]
@@ -157,6 +177,7 @@ def microsteps(args):
         loss.backward()
         model.zero_grad(set_to_none=True)
     torch.cuda.synchronize()
+    log("[microsteps] done")
 
 
 def main():
@@ -182,6 +203,9 @@ def main():
 
     rank, world, local = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(
         os.environ.get("LOCAL_RANK", 0))
+    traffic = {}
+    if rank == 0 and world == 1 and not args.no_traffic and not args.no_profile:
+        traffic = pmc_traffic(args)  # before this process initialises the GPU
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -294,12 +318,10 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
                 "launches_per_microstep": n, "avg_launch_ms": round(ms / n, 4),
                 "share_of_microstep_kernel_time": round(ms / tot_ms, 3)}
-        # HBM bytes per launch of the same kernel, measured now on this box (PMC passes in child
-        # processes over one micro-step of the same model)
-        if rank == 0 and world == 1 and not args.no_traffic:
-            torch.cuda.synchronize()
-            torch.cuda.empty_cache()
-            tr = live_traffic(dom, args)
+        # HBM bytes per launch of the same kernel, measured in this run on this box (PMC passes in
+        # child processes over one micro-step of the same model, pmc_traffic)
+        if traffic.get(dom):
+            tr = traffic[dom]
             if tr:
                 roof["traffic"] = round(tr["bytes"])
                 roof["traffic_unit"] = "bytes/launch (HBM, PMC, this run)"

@@ -419,21 +419,39 @@ __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R,
   for (int e = 0; e < 8; ++e) atomicAdd(out + col + e, acc[e]);
 }
 
-// out[n] += sum_s part[s][n] in split order (N % 4 == 0); shared with the GEMM's fused column sums
+// out[n] += sum_s part[s][n] (N % 4 == 0); shared with the GEMM's fused column sums.  A block is 64
+// columns (16 quads) x 16 split lanes: lane sl adds splits sl, sl + 16, ... in order with 8 loads in
+// flight (a single thread walking hundreds of splits is latency-bound), then the 16 lane sums meet
+// in a fixed LDS tree -- the result depends only on (splits, N), never on timing.
 __global__ __launch_bounds__(256) void colsum_reduce_k(const float* __restrict__ part, int splits, long N,
-                                                            float* __restrict__ out) {
-  const long n = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (n >= N) return;
-  f32x4 a = *(const f32x4*)(part + n);
-  for (int sp = 1; sp < splits; ++sp) {
-    const f32x4 b = *(const f32x4*)(part + (long)sp * N + n);
+                                                       float* __restrict__ out) {
+  __shared__ f32x4 red[16][16];
+  const int cq = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const long n = ((long)blockIdx.x * 16 + cq) * 4;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int sp = sl;
+    for (; sp + 16 * 7 < splits; sp += 16 * 8) {
+      f32x4 v[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) a[e] += b[e];
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(part + (long)(sp + 16 * u) * N + n);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; sp < splits; sp += 16) a += *(const f32x4*)(part + (long)sp * N + n);
   }
-  f32x4 o = *(f32x4*)(out + n);
+  red[sl][cq] = a;
+  __syncthreads();
 #pragma unroll
-  for (int e = 0; e < 4; ++e) o[e] += a[e];
-  *(f32x4*)(out + n) = o;
+  for (int w = 8; w >= 1; w >>= 1) {
+    if (sl < w) red[sl][cq] += red[sl + w][cq];
+    __syncthreads();
+  }
+  if (sl == 0 && n < N) {
+    f32x4 o = *(f32x4*)(out + n);
+    o += red[0][cq];
+    *(f32x4*)(out + n) = o;
+  }
 }
 
 // ------------------------------------------------------------------ attention-bwd preprocess
@@ -590,7 +608,7 @@ extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, fl
 }
 
 int owlk::colsum_reduce(const float* part, int splits, long N, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_reduce_k, dim3((unsigned)((N / 4 + 255) / 256)), dim3(256), 0, s, part, splits, N, out);
+  hipLaunchKernelGGL(colsum_reduce_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, part, splits, N, out);
   return owlk::check_launch("colsum_reduce");
 }
 
