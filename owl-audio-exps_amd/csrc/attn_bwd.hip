@@ -365,6 +365,253 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
   }
 }
 
+// ======================================================================== dK, dV on 16x16x32 MFMAs
+// The same workgroup, ring and tile classes as attn_bwd_dkdv_k (D 64), with every product on
+// v_mfma_f32_16x16x32_bf16: the chip holds a higher clock on that shape than on 32x32x16 at the same
+// cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7).  Per wave 32 keys as two 16-key
+// column tiles (lane column c = lane & 15, k-group g = lane >> 4); per 32-query block two 16-row
+// tiles.  S and dP put the key on the lane column and the query on rows 4 g + r, so their
+// accumulators are the B operands of dV^T += dO^T P and dK^T += Q^T dS with the k (query) order
+// permuted: slot j of group g is query 4 g + j (j < 4) or 16 + 4 g + (j - 4); the A operands dO^T
+// and Q^T are read in that order by two ds_read_b64_tr_b16 per fragment (rows 4 g .. 4 g + 3 and
+// 16 + 4 g .. + 3 of the tile, columns 16 ds + 4 (c & 3) .. + 3).
+template <int QT_>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(BwdP p) {
+  constexpr int D = 64;
+  using G = DkdvCfg<D, QT_>;
+  constexpr int QT = G::QT, TLQ = G::TLQ, NBUF = G::NBUF;
+  constexpr int BUF = 2 * QT * SUB + 2 * TLQ * 4;  // Q [QT] | dO [QT] | lse2 | delta
+  constexpr int LSEW = TLQ / 64;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + 16];
+  int& red_hi = *(int*)(smem + NBUF * BUF);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const BlockIds bid = xcd_block_ids();
+  const long b = bid.z;
+  const int head = bid.y;
+  const long k0 = (long)bid.x * TB;
+  const long kw0 = k0 + 32 * w;
+  const MaskP& m = p.m;
+
+  const bf16* Q = p.q + b * p.sqb + head * D;
+  const bf16* K = p.k + b * p.skb + head * D;
+  const bf16* V = p.v + b * p.svb + head * D;
+  const bf16* dO = p.dout + b * p.sob + head * D;
+  const float* LSE = p.lse + (b * p.H + head) * p.Lq;
+  const float* DLT = p.delta + (b * p.H + head) * p.Lq;
+
+  const long klast = (k0 + TB < p.Lkv ? k0 + TB : p.Lkv) - 1;
+  const int fk_lo = frame_of(m, k0), fk_hi = frame_of(m, klast);
+  int fq_end;
+  if (m.q_hi) {
+    if (threadIdx.x == 0) red_hi = -1;
+    __syncthreads();
+    int mx = -1;
+    for (int f = fk_lo + threadIdx.x; f <= fk_hi; f += 256) mx = max(mx, m.q_hi[b * m.fstride + f]);
+    atomicMax(&red_hi, mx);
+    __syncthreads();
+    fq_end = red_hi;
+  } else {
+    fq_end = m.window > 0 ? min(m.n_frames - 1, fk_hi + m.window - 1) : m.n_frames - 1;
+  }
+  const int fq_start = m.causal ? fk_lo : (m.window > 0 ? max(0, fk_lo - m.window + 1) : 0);
+  long qbeg = ((long)fq_start * m.tpf / TL) * TL;
+  long qend = ((long)fq_end + 1) * m.tpf;
+  if (qend > p.Lq) qend = p.Lq;
+  const int ntiles = qend > qbeg ? (int)((qend - qbeg + TLQ - 1) / TLQ) : 0;
+
+  // this lane's two keys (column c of the wave's two 16-key tiles) as B operands, k' = bf16(-c k),
+  // v' = -v (row constants in the accumulators, as attn_bwd_dkdv_k)
+  long my_k[2];
+  bf16x8 kf[2][2], vf[2][2];  // [key tile][k step of 32 d]
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    my_k[t2] = kw0 + 16 * t2 + c;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 kv = my_k[t2] < p.Lkv ? *(const bf16x8*)(K + my_k[t2] * p.ldk + 32 * ks + 8 * g) : bf16x8{};
+      bf16x8 vv = my_k[t2] < p.Lkv ? *(const bf16x8*)(V + my_k[t2] * p.ldv + 32 * ks + 8 * g) : bf16x8{};
+      float f[8], h8[8];
+      unpack8(kv, f);
+      unpack8(vv, h8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] *= -p.scale_log2;
+        h8[j] = -h8[j];
+      }
+      kf[t2][ks] = pack8(f);
+      vf[t2][ks] = pack8(h8);
+    }
+  }
+  const bool wave_live = kw0 < p.Lkv;
+  const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
+  const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
+  TileRange full = full_range_q(m, b, wfk0, wfk1, qbeg, p.Lq, TLQ);
+  if (!wave_live || kw0 + 32 > p.Lkv) full = TileRange{1, 0};
+  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
+  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
+
+  f32x4 dk[4][2], dv[4][2];  // [16-column d tile][key tile]
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) dk[ds][t2] = dv[ds][t2] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const GldsOff go_q = glds_offsets<SW_DUAL>(p.ldq, w, lane), go_d = glds_offsets<SW_DUAL>(p.ldo, w, lane);
+  auto issue = [&](char* buf, long q0) {
+#pragma unroll
+    for (int sq = 0; sq < QT; ++sq) {
+      const long r = q0 + 64 * sq;
+      char* bq = buf + sq * SUB;
+      char* bd = buf + (QT + sq) * SUB;
+      if (r + TL <= p.Lq) {
+        tile_glds_fast(bq, Q + r * p.ldq, go_q, w);
+        tile_glds_fast(bd, dO + r * p.ldo, go_d, w);
+      } else {
+        tile_glds<SW_DUAL>(bq, Q, p.ldq, r, p.Lq, w, lane);
+        tile_glds<SW_DUAL>(bd, dO, p.ldo, r, p.Lq, w, lane);
+      }
+    }
+    if (w < 2 * LSEW) {
+      const int part = w >> 1;
+      const long r = q0 + 64 * part;
+      const long n = p.Lq - r;
+      const int i = r + 64 <= p.Lq ? lane : (lane < n ? lane : (n > 0 ? (int)n - 1 : 0));
+      const long src = r + i < p.Lq ? r + i : p.Lq - 1;
+      glds_f32(buf + 2 * QT * SUB + ((w & 1) * TLQ + 64 * part) * 4, ((w & 1) ? DLT : LSE) + src);
+    }
+  };
+  constexpr int OPS = 4 * QT;
+  auto wait_oldest = [&](int younger) {
+    if (younger <= 0)
+      vmcnt<0>();
+    else if (w < 2 * LSEW)
+      vmcnt<OPS + 1>();
+    else
+      vmcnt<OPS>();
+  };
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * BUF, qbeg + (long)i * TLQ);
+  wait_oldest(min(NBUF - 2, ntiles - 1));
+  OWLK_BARRIER();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const long q0 = qbeg + (long)t * TLQ;
+    if (t + NBUF - 1 < ntiles) issue(smem + ((t + NBUF - 1) % NBUF) * BUF, q0 + (long)(NBUF - 1) * TLQ);
+    const char* tb = smem + (t % NBUF) * BUF;
+    const float* l2 = (const float*)(tb + 2 * QT * SUB);
+    const float* dlt = l2 + TLQ;
+
+    int kind = TILE_FULL;
+    if (t < full.lo || t >= full.hi) {
+      const long qlast = (q0 + TLQ - 1 < p.Lq ? q0 + TLQ - 1 : p.Lq - 1);
+      kind = TILE_EMPTY;
+      if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
+      if (kind == TILE_FULL && (q0 + TLQ > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
+    }
+    kind = __builtin_amdgcn_readfirstlane(kind);
+
+    if (kind != TILE_EMPTY) {
+      const bool masked = kind == TILE_PARTIAL;
+#pragma unroll
+      for (int sq = 0; sq < QT; ++sq) {
+        const char* lq = tb + sq * SUB;
+        const char* ld = tb + (QT + sq) * SUB;
+        unsigned long long bh[2] = {0ull, 0ull};
+        if (masked) {
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2)
+            bh[t2] = tile_bits(m, b, my_k[t2], my_k[t2] < p.Lkv, q0 + 64 * sq, p.Lq, false) >> (4 * g);
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          f32x4 st[2][2], dp[2][2];  // [16-row query tile][key tile]
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs) {
+            const int rowb = 64 * sq + 32 * qb + 16 * qs + 4 * g;
+            const f32x4 L = *(const f32x4*)(l2 + rowb);
+            const f32x4 Dl = *(const f32x4*)(dlt + rowb);
+            st[qs][0] = st[qs][1] = L;
+            dp[qs][0] = dp[qs][1] = Dl;
+          }
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+              const bf16x8 aq = frag_row16(lq, 32 * qb + 16 * qs, ks, lane);
+              const bf16x8 ad = frag_row16(ld, 32 * qb + 16 * qs, ks, lane);
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2) {
+                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kf[t2][ks], st[qs][t2], 0, 0, 0);
+                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vf[t2][ks], dp[qs][t2], 0, 0, 0);
+              }
+            }
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
+          if (masked) {
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2) {
+              if (qb == 0) {
+                apply_bits4<0>(st[0][t2], bh[t2], 0.f);
+                apply_bits4<16>(st[1][t2], bh[t2], 0.f);
+              } else {
+                apply_bits4<32>(st[0][t2], bh[t2], 0.f);
+                apply_bits4<48>(st[1][t2], bh[t2], 0.f);
+              }
+            }
+          }
+          bf16x8 pf[2], sf[2];
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) {
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) dp[qs][t2][r] *= st[qs][t2][r];
+            pf[t2] = pack_perm(st[0][t2], st[1][t2]);
+            sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
+          }
+#pragma unroll
+          for (int ds = 0; ds < 4; ++ds) {
+            const bf16x8 ado = frag_tr16(ld, 32 * qb, ds, lane);
+            const bf16x8 aqt = frag_tr16(lq, 32 * qb, ds, lane);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2) {
+              dv[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pf[t2], dv[ds][t2], 0, 0, 0);
+              dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+    wait_oldest(min(NBUF - 2, ntiles - 2 - t));
+    OWLK_BARRIER();
+  }
+
+  // dK[key][d], dV[key][d]: this lane holds d = 16 ds + 4 g + r of its two keys
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    if (my_k[t2] >= p.Lkv) continue;
+    bf16* pk = p.dk + b * p.sdkb + my_k[t2] * p.lddk + head * D + 4 * g;
+    bf16* pv = p.dv + b * p.sdvb + my_k[t2] * p.lddv + head * D + 4 * g;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      bf16x4 a4, b4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a4[e] = (bf16)(dk[ds][t2][e] * -p.scale);  // dS was accumulated negated
+        b4[e] = (bf16)dv[ds][t2][e];
+      }
+      *(bf16x4*)(pk + 16 * ds) = a4;
+      *(bf16x4*)(pv + 16 * ds) = b4;
+    }
+  }
+}
+
 // ======================================================================== dQ
 // Key tiles of QT x 64 rows per ring slot: QT = 2 (D 64, unwindowed masks; two-slot ring) pays the
 // per-tile fixed costs once per 48 MFMAs, as in the dK/dV kernel.
@@ -547,15 +794,236 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
   if (qok) store_rowT<C::NDB>(p.dq + b * p.sdqb + my_q * p.lddq + head * D, dq, p.scale, h);
 }
 
+// ======================================================================== dQ on 16x16x32 MFMAs
+// attn_bwd_dq_k (D 64, accumulator-init form) with every product on v_mfma_f32_16x16x32_bf16
+// (see attn_bwd_dkdv16_k): per wave 32 queries as two 16-query column tiles (lane column c), per
+// 32-key block two 16-row key tiles; S and dP take K / V rows from LDS as A and q' = bf16(c q) /
+// dO from registers as B, so their accumulators (key on rows 4 g + r) are the B operands of
+// dQ^T += K^T dS in the permuted key order, K^T read by two ds_read_b64_tr_b16 per fragment.
+template <int QT>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
+  constexpr int D = 64;
+  constexpr int NBUF = QT == 2 ? 2 : Cfg<D>::NBUF, TLK = TL * QT;
+  constexpr int BUF = 2 * QT * SUB;  // K [QT] | V [QT]
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + 16];
+  int& red_lo = *(int*)(smem + NBUF * BUF);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const BlockIds bid = xcd_block_ids();
+  const long b = bid.z;
+  const int head = bid.y;
+  const int ntq = (int)((p.Lq + TB - 1) / TB);
+  const long q0 = (long)(ntq - 1 - bid.x) * TB;
+  const long r0 = q0 + 32 * w;
+  const MaskP& m = p.m;
+
+  const bf16* Q = p.q + b * p.sqb + head * D;
+  const bf16* K = p.k + b * p.skb + head * D;
+  const bf16* V = p.v + b * p.svb + head * D;
+  const bf16* dO = p.dout + b * p.sob + head * D;
+
+  const long qlast = (q0 + TB < p.Lq ? q0 + TB : p.Lq) - 1;
+  const int fq_lo = frame_of(m, q0 + m.q_offset), fq_hi = frame_of(m, qlast + m.q_offset);
+  int lo_f;
+  if (m.kv_lo) {
+    if (threadIdx.x == 0) red_lo = 1 << 30;
+    __syncthreads();
+    int mn = 1 << 30;
+    for (int f = fq_lo + threadIdx.x; f <= fq_hi; f += 256) mn = min(mn, m.kv_lo[b * m.fstride + f]);
+    atomicMin(&red_lo, mn);
+    __syncthreads();
+    lo_f = red_lo;
+  } else {
+    lo_f = m.window > 0 ? max(0, fq_lo - m.window + 1) : 0;
+  }
+  const int hi_f = m.causal ? fq_hi : (m.window > 0 ? min(m.n_frames - 1, fq_hi + m.window - 1) : m.n_frames - 1);
+  long kv_begin = ((long)lo_f * m.tpf / TL) * TL;
+  long kv_end = ((long)hi_f + 1) * m.tpf;
+  if (kv_end > p.Lkv) kv_end = p.Lkv;
+  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + TLK - 1) / TLK) : 0;
+
+  long my_q[2];
+  bool qok[2];
+  bf16x8 qf[2][2], df[2][2];  // [query tile][k step of 32 d]
+  f32x4 sinit[2], pinit[2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    my_q[t2] = r0 + 16 * t2 + c;
+    qok[t2] = my_q[t2] < p.Lq;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 qv = qok[t2] ? *(const bf16x8*)(Q + my_q[t2] * p.ldq + 32 * ks + 8 * g) : bf16x8{};
+      df[t2][ks] = qok[t2] ? *(const bf16x8*)(dO + my_q[t2] * p.ldo + 32 * ks + 8 * g) : bf16x8{};
+      float f[8];
+      unpack8(qv, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= p.scale_log2;
+      qf[t2][ks] = pack8(f);
+    }
+    const float L2 = qok[t2] ? p.lse[(b * p.H + head) * p.Lq + my_q[t2]] : 0.f;
+    const float Dl = qok[t2] ? p.delta[(b * p.H + head) * p.Lq + my_q[t2]] : 0.f;
+    sinit[t2] = f32x4{-L2, -L2, -L2, -L2};
+    pinit[t2] = f32x4{-Dl, -Dl, -Dl, -Dl};
+  }
+  const bool wave_live = r0 < p.Lq;
+  const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
+  const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
+  TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, TLK);
+  if (!wave_live) full = TileRange{1, 0};
+  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
+  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
+
+  f32x4 dq[4][2];  // [16-row d tile][query tile]
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) dq[ds][0] = dq[ds][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const GldsOff go_k = glds_offsets<SW_DUAL>(p.ldk, w, lane), go_v = glds_offsets<SW_ROW>(p.ldv, w, lane);
+  auto issue = [&](char* buf, long c0) {
+#pragma unroll
+    for (int sk = 0; sk < QT; ++sk) {
+      const long cc = c0 + 64 * sk;
+      char* bk = buf + sk * SUB;
+      char* bv = buf + (QT + sk) * SUB;
+      if (cc + TL <= p.Lkv) {
+        tile_glds_fast(bk, K + cc * p.ldk, go_k, w);
+        tile_glds_fast(bv, V + cc * p.ldv, go_v, w);
+      } else {
+        tile_glds<SW_DUAL>(bk, K, p.ldk, cc, p.Lkv, w, lane);
+        tile_glds<SW_ROW>(bv, V, p.ldv, cc, p.Lkv, w, lane);
+      }
+    }
+  };
+  constexpr int OPS = 4 * QT;
+  auto wait_oldest = [&](int younger) {
+    if (younger > 0)
+      vmcnt<OPS>();
+    else
+      vmcnt<0>();
+  };
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * BUF, kv_begin + (long)i * TLK);
+  wait_oldest(min(NBUF - 2, ntiles - 1));
+  OWLK_BARRIER();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const long c0 = kv_begin + (long)t * TLK;
+    if (t + NBUF - 1 < ntiles) issue(smem + ((t + NBUF - 1) % NBUF) * BUF, c0 + (long)(NBUF - 1) * TLK);
+    const char* tb = smem + (t % NBUF) * BUF;
+    int kind = TILE_FULL;
+    if (t < full.lo || t >= full.hi) {
+      const long clast = (c0 + TLK - 1 < p.Lkv ? c0 + TLK - 1 : p.Lkv - 1);
+      kind = TILE_EMPTY;
+      if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
+      if (kind == TILE_FULL && c0 + TLK > p.Lkv) kind = TILE_PARTIAL;
+    }
+    kind = __builtin_amdgcn_readfirstlane(kind);
+
+    if (kind != TILE_EMPTY) {
+      const bool masked = kind == TILE_PARTIAL;
+#pragma unroll
+      for (int sk = 0; sk < QT; ++sk) {
+        const char* lk = tb + sk * SUB;
+        const char* lv = tb + (QT + sk) * SUB;
+        unsigned long long bh[2] = {0ull, 0ull};
+        if (masked) {
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2)
+            bh[t2] = tile_bits(m, b, my_q[t2], qok[t2], c0 + 64 * sk, p.Lkv, true) >> (4 * g);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          f32x4 st[2][2], dp[2][2];  // [16-row key tile][query tile]
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2) {
+              st[ks][t2] = sinit[t2];
+              dp[ks][t2] = pinit[t2];
+            }
+#pragma unroll
+          for (int kd = 0; kd < 2; ++kd)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              const bf16x8 ak = frag_row16<SW_DUAL>(lk, 32 * kb + 16 * ks, kd, lane);
+              const bf16x8 av = frag_row16<SW_ROW>(lv, 32 * kb + 16 * ks, kd, lane);
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2) {
+                st[ks][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t2][kd], st[ks][t2], 0, 0, 0);
+                dp[ks][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df[t2][kd], dp[ks][t2], 0, 0, 0);
+              }
+            }
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) st[ks][t2][r] = __builtin_amdgcn_exp2f(st[ks][t2][r]);
+          if (masked) {
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2) {
+              if (kb == 0) {
+                apply_bits4<0>(st[0][t2], bh[t2], 0.f);
+                apply_bits4<16>(st[1][t2], bh[t2], 0.f);
+              } else {
+                apply_bits4<32>(st[0][t2], bh[t2], 0.f);
+                apply_bits4<48>(st[1][t2], bh[t2], 0.f);
+              }
+            }
+          }
+          bf16x8 sf[2];
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) dp[ks][t2][r] *= st[ks][t2][r];
+            sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
+          }
+#pragma unroll
+          for (int ds = 0; ds < 4; ++ds) {
+            const bf16x8 akt = frag_tr16(lk, 32 * kb, ds, lane);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+              dq[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akt, sf[t2], dq[ds][t2], 0, 0, 0);
+          }
+        }
+      }
+    }
+    wait_oldest(min(NBUF - 2, ntiles - 2 - t));
+    OWLK_BARRIER();
+  }
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    if (!qok[t2]) continue;
+    bf16* pq = p.dq + b * p.sdqb + my_q[t2] * p.lddq + head * D + 4 * g;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      bf16x4 a4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a4[e] = (bf16)(dq[ds][t2][e] * p.scale);
+      *(bf16x4*)(pq + 16 * ds) = a4;
+    }
+  }
+}
+
 template <int D>
 int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipStream_t s) {
   if (phases & 1) {
     const dim3 grid((unsigned)((Lkv + TB - 1) / TB), (unsigned)H, (unsigned)B);
     if constexpr (D == 64) {
-      if (p.m.window <= 0)
+      // the 16x16x32-MFMA variant by default (OWLK_DKDV16 = 0: 32x32x16): -7 % at the dit_v4 shape
+      static const int v16 = getenv("OWLK_DKDV16") ? atoi(getenv("OWLK_DKDV16")) : 1;
+      if (v16) {
+        if (p.m.window <= 0)
+          hipLaunchKernelGGL((attn_bwd_dkdv16_k<2>), grid, dim3(256), 0, s, p);
+        else
+          hipLaunchKernelGGL((attn_bwd_dkdv16_k<1>), grid, dim3(256), 0, s, p);
+      } else if (p.m.window <= 0) {
         hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2>), grid, dim3(256), 0, s, p);
-      else
+      } else {
         hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 1>), grid, dim3(256), 0, s, p);
+      }
     } else {
       // D 128 (one wave per SIMD): OWLK_DKDV128 = 0 plain, 1 pipelined FULL tiles, 2 128-row
       // query tiles (two-slot ring, 130 KiB), 3 both (default; global 134.7 -> 99.6 ms, local
@@ -576,10 +1044,17 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
   if (phases & 2) {
     const dim3 grid((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B);
     if constexpr (D == 64) {
-      if (p.m.window <= 0)
+      static const int v16 = getenv("OWLK_DQ16") ? atoi(getenv("OWLK_DQ16")) : 1;  // 16x16x32 variant (0: 32x32x16)
+      if (v16) {
+        if (p.m.window <= 0)
+          hipLaunchKernelGGL((attn_bwd_dq16_k<2>), grid, dim3(256), 0, s, p);
+        else
+          hipLaunchKernelGGL((attn_bwd_dq16_k<1>), grid, dim3(256), 0, s, p);
+      } else if (p.m.window <= 0) {
         hipLaunchKernelGGL((attn_bwd_dq_k<D, 2>), grid, dim3(256), 0, s, p);
-      else
+      } else {
         hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
+      }
     } else {
       hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
     }

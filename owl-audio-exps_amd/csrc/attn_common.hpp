@@ -243,6 +243,50 @@ DEV bf16x8 frag_tr(const char* lds, int row0, int s, int cb, int lane) {
   return join_tr(lo, hi);
 }
 
+// ---- v_mfma_f32_16x16x32_bf16 forms (lane column c = lane & 15, k-group / row group g = lane >> 4;
+// C/D element r of lane (c, g) is row 4 g + r, column c).  An accumulator tile feeds the next
+// product as its B operand with the k order permuted: slot j of group g is row 4 g + j (j < 4) of
+// the first 16-row tile and 4 g + (j - 4) of the second; the other operand is read in that order.
+template <int BASE>
+DEV void apply_bits4(f32x4& a, unsigned long long bh, float fill) {
+  __asm__ volatile("");  // keeps the caller's uniform branch a branch
+  const unsigned w = (unsigned)(bh >> BASE);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) a[r] = (w >> r) & 1u ? a[r] : fill;
+}
+
+// 16x16x32 A fragment read row-wise: row = row0 + (lane & 15), k = 32 ks + 8 (lane >> 4) .. + 7
+template <int S = SW_DUAL>
+DEV bf16x8 frag_row16(const char* lds, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 15);
+  return *(const bf16x8*)(lds + r * 128 + (((4 * ks + (lane >> 4)) ^ swz<S>(r)) << 4));
+}
+
+// 16x16x32 A fragment of X^T in the permuted k order: element j of lane (c = lane & 15,
+// g = lane >> 4) = tile[row0 + 4 g + (j & 3) + 16 (j >> 2)][16 ds + c], by two ds_read_b64_tr_b16
+// (rows 4 g .. 4 g + 3 and 16 + 4 g .. + 3, columns 16 ds + 4 (c & 3) .. + 3 addressed by lane c)
+template <int S = SW_DUAL>
+DEV bf16x8 frag_tr16(const char* lds, int row0, int ds, int lane) {
+  const int c = lane & 15, g = lane >> 4;
+  const int ra = row0 + 4 * g + (c >> 2), rb_ = ra + 16;
+  const int ch = 2 * ds + ((c & 3) >> 1);
+  const s16x4 lo = ds_read_tr16(lds + ra * 128 + ((ch ^ swz<S>(ra)) << 4) + 8 * (c & 1));
+  const s16x4 hi = ds_read_tr16(lds + rb_ * 128 + ((ch ^ swz<S>(rb_)) << 4) + 8 * (c & 1));
+  return join_tr(lo, hi);
+}
+
+// two 16x16 accumulator tiles stacked along k (rows 4 g + r of tile 0, then of tile 1) -> the
+// bf16 B fragment in the permuted k order frag_tr16 reads its A operand in
+DEV bf16x8 pack_perm(const f32x4& a0, const f32x4& a1) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[j] = (bf16)a0[j];
+    f[4 + j] = (bf16)a1[j];
+  }
+  return f;
+}
+
 // accumulator registers 8 s .. 8 s + 7 of a 32x32 tile -> bf16 B fragment for k-step s
 DEV bf16x8 acc_frag(const f32x16& a, int s) {
   bf16x8 f;
