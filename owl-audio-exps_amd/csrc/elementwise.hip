@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
           unpack8(*(const bf16x8*)(ypre + row * lddy + c * 8), yp);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float sg = 1.f / (1.f + __expf(-yp[e]));
+            const float sg = sigmoid_f(yp[e]);
             dv[e] = rb(dv[e] * sg * (1.f + yp[e] * (1.f - sg)));
           }
         }

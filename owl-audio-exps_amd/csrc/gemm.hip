@@ -40,6 +40,7 @@ struct GemmP {
   const float* bias;
   bf16* aux; long ldaux, sAux;
   const bf16* gate; long ldgate, sGate, tpf;
+  unsigned tpf_mul; int tpf_shift;  // row / tpf = tpf_mul ? umulhi(row, tpf_mul) >> tpf_shift : row >> tpf_shift
   const bf16* resid; long ldres, sRes;
   int tiles_m, tiles_n;
   long kchunk;  // split-K: K range per blockIdx.y (multiple of BK)
@@ -138,6 +139,12 @@ DEV bf16x8 read_frag_async(const char* lds, int row0, int kk, int lane) {
 }
 
 // epilogue for 8 consecutive outputs C[gm, gn .. gn + 8) of batch item z (v = raw accumulators)
+// row -> frame (gate row) without an integer division: tpf_mul = ceil(2^(32+s) / tpf), s = floor(log2 tpf),
+// exact for rows < 2^31 (the error m*tpf - 2^(32+s) < tpf <= 2^(s+1) times the row stays under 2^(32+s))
+DEV unsigned frame_of(const GemmP& p, unsigned row) {
+  return p.tpf_mul ? __umulhi(row, p.tpf_mul) >> p.tpf_shift : row >> p.tpf_shift;
+}
+
 template <int EPI, bool OF32>
 DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
   float bb[8];
@@ -181,7 +188,7 @@ DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
     float y[8], g[8], r[8], o[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) y[e] = rb(v[e] + bb[e]);
-    unpack8(*(const bf16x8*)(p.gate + z * p.sGate + (gm / p.tpf) * p.ldgate + gn), g);
+    unpack8(*(const bf16x8*)(p.gate + z * p.sGate + (long)frame_of(p, (unsigned)gm) * p.ldgate + gn), g);
     unpack8(*(const bf16x8*)(p.resid + z * p.sRes + gm * p.ldres + gn), r);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = r[e] + rb(g[e] * y[e]);
@@ -192,7 +199,7 @@ DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
     unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float sg = 1.f / (1.f + __expf(-x[e]));
+      const float sg = sigmoid_f(x[e]);
       o[e] = rb(v[e]) * sg * (1.f + x[e] * (1.f - sg));
     }
     *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
@@ -271,7 +278,7 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
     unpack8(x, xx);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float sg = 1.f / (1.f + __expf(-xx[e]));
+      const float sg = sigmoid_f(xx[e]);
       o[e] = rb(v[e]) * sg * (1.f + xx[e] * (1.f - sg));
     }
     st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
@@ -753,7 +760,7 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
                                                  : p.aux + z * p.sAux + gm * p.ldaux;
         x[q] = *(const bf16x8*)(src + gn);
       }
-      if (HAS_G) g[q] = *(const bf16x8*)(p.gate + z * p.sGate + (long)((unsigned)gm / (unsigned)p.tpf) * p.ldgate + gn);
+      if (HAS_G) g[q] = *(const bf16x8*)(p.gate + z * p.sGate + (long)frame_of(p, (unsigned)gm) * p.ldgate + gn);
     }
   };
   if (!atomic) {
@@ -1083,6 +1090,7 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   OWLK_REQUIRE(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0, "gemm: operands must be 16-byte aligned");
   OWLK_REQUIRE(!c_f32 || epi == EPI_STORE, "gemm: fp32 output only with EPI_STORE");
   OWLK_REQUIRE(epi != EPI_GATE_RESID || (gate && resid && tpf > 0), "gemm: gate epilogue needs gate/resid/tpf");
+  OWLK_REQUIRE(epi != EPI_GATE_RESID || M < (1L << 31), "gemm: gate epilogue rows must stay below 2^31");
   OWLK_REQUIRE(!(epi == EPI_SILU || epi == EPI_DSILU || epi == EPI_AXPBY || epi == EPI_SCALE2) || aux,
                "gemm: epilogue needs aux");
   OWLK_REQUIRE(epi != EPI_SCALE2 || (!a_trans && !b_trans), "gemm: SCALE2 epilogue needs k-contiguous operands");
@@ -1093,6 +1101,12 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   p.alpha = alpha; p.beta = beta; p.bias = bias;
   p.aux = (bf16*)aux; p.ldaux = ldaux; p.sAux = sAux;
   p.gate = (const bf16*)gate; p.ldgate = ldgate; p.sGate = sGate; p.tpf = tpf > 0 ? tpf : 1;
+  {
+    int sh = 0;
+    while ((2L << sh) <= p.tpf) ++sh;
+    p.tpf_shift = sh;
+    p.tpf_mul = (p.tpf & (p.tpf - 1)) ? (unsigned)(((1ULL << (32 + sh)) + p.tpf - 1) / p.tpf) : 0u;
+  }
   p.resid = (const bf16*)resid; p.ldres = ldres; p.sRes = sRes;
   hipStream_t s = (hipStream_t)stream;
   const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;

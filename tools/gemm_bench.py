@@ -54,6 +54,24 @@ def main():
         ref = timeit(lambda: torch.matmul(Am, Bm))
         print(f"{name:8s} [{M}x{N}x{Kd}]  owlk {ours:7.3f} ms {fl / ours / 1e9:7.1f} TF/s | "
               f"hipBLASLt {ref:7.3f} ms {fl / ref / 1e9:7.1f} TF/s", flush=True)
+    # fused epilogues at the block's shapes (fused.py): fc1 + SiLU, fc1 dX + dSiLU + bias-grad colsum,
+    # out-proj / fc2 + gate + residual
+    x, w1, w2, wo = r(T, d), r(4 * d, d), r(d, 4 * d), r(d, d)
+    h, dy = r(T, 4 * d), r(T, d)
+    aux4, aux1 = torch.empty_like(h), torch.empty_like(dy)
+    b4, b1 = torch.zeros(4 * d, device="cuda"), torch.zeros(d, device="cuda")
+    gate, cs = r(T // 64, d), torch.zeros(4 * d, device="cuda")
+    epis = [
+        ("fc1 silu", 2.0 * T * 4 * d * d, lambda: K.gemm(x, w1, epi=K.EPI_SILU, bias=b4, aux=aux4)),
+        ("fc1 dsilu", 2.0 * T * 4 * d * d, lambda: K.gemm(dy, w2, b_trans=True, epi=K.EPI_DSILU, aux=h, colsum=cs)),
+        ("fc2 gate", 2.0 * T * d * 4 * d, lambda: K.gemm(h, w2, epi=K.EPI_GATE_RESID, bias=b1, aux=aux1, gate=gate,
+                                                        tpf=64, resid=dy)),
+        ("out gate", 2.0 * T * d * d, lambda: K.gemm(x, wo, epi=K.EPI_GATE_RESID, bias=b1, aux=aux1, gate=gate,
+                                                    tpf=64, resid=dy)),
+    ]
+    for name, fl, fn in epis:
+        ours = timeit(fn)
+        print(f"{name:9s} owlk {ours:7.3f} ms {fl / ours / 1e9:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
