@@ -35,10 +35,18 @@ int owlk_device_ok(void);
  *   aligned) the per-split partials go there and one fixed-order reduce forms C: the result is
  *   bitwise deterministic.  Without it (ws null or too small) the splits combine by fp32 atomics
  *   onto C (cleared first when beta = 0).  The library never allocates.
+ *   Decode plan (M <= 128, batch 1, a_trans = b_trans = 0, bf16 C, STORE / SILU / GATE_RESID,
+ *   N % 64 == 0, K % 32 == 0): one launch of 64-column tiles with K split over workgroups; the last
+ *   workgroup of a tile adds the chunks' partials in order (deterministic).  When
+ *   owlk_gemm_ws_bytes reports a non-zero size for it, the first OWLK_DECODE_COUNTER_BYTES of ws
+ *   are per-tile arrival counters that MUST be zero on entry; every launch leaves them zero, so
+ *   keep one zero-initialised workspace per device and do not share it between concurrent
+ *   streams.  Without a large enough workspace the call takes the 64^2-tile path.
  *   colsum (optional, batch 1, bf16 C): colsum[n] += sum_m C[m, n] over the stored bf16 values
  *   (bias gradient of the next layer, fused into the DSILU epilogue of the 256^2 kernel; a
  *   separate column-sum pass otherwise); deterministic with the workspace (per-tile partial rows
  *   added in order), fp32 atomics without.  It accumulates onto colsum. */
+#define OWLK_DECODE_COUNTER_BYTES 4096
 int owlk_gemm(long M, long N, long K, long batch,
               const void* A, long lda, long sA, int a_trans,
               const void* B, long ldb, long sB, int b_trans,
@@ -55,6 +63,10 @@ long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int
  * the column-sum partials (fused or separate pass) */
 long owlk_gemm_ws_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                         float beta, int colsum);
+/* leading bytes of that workspace that must be zero on entry (the decode plan's arrival counters,
+ * OWLK_DECODE_COUNTER_BYTES; every launch leaves them zero); 0 when the plan keeps no state in ws */
+long owlk_gemm_ws_counter_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
+                                float beta);
 
 /* ---- AdaLN modulate (modulation.py:7-26 AdaLN.forward after its fc; :46-55 cond_adaln):
  *   y[t] = bf16(bf16(bf16(rms_norm(x[t])) * bf16(1 + scale[t/tpf])) + shift[t/tpf]); rstd[t] fp32 */

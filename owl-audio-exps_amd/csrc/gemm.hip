@@ -48,6 +48,7 @@ struct GemmP {
   float* colsum_req;  // caller wants colsum[n] += sum_m C[m, n] (stored bf16 values)
   float* colsum;      // ... and the launched kernel fuses it (set by the dispatch, else a separate pass)
   float* cs_part;     // fused column sums as per-(tile row, wave row) partials [tiles_m * 2][N] (deterministic)
+  int group_m;        // gemm_pp_kernel tile order: groups of group_m tile rows (<= 1: row-major)
 };
 
 // 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
@@ -149,7 +150,15 @@ template <int EPI, bool OF32>
 DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
   float bb[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bb[e] = p.bias ? rb(p.bias[gn + e]) : 0.f;
+  for (int e = 0; e < 8; ++e) bb[e] = 0.f;
+  if (p.bias) {  // two 16-B loads (gn % 8 == 0), not eight dependent scalar ones
+    const f32x4 lo = *(const f32x4*)(p.bias + gn), hi = *(const f32x4*)(p.bias + gn + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bb[e] = rb(lo[e]);
+      bb[e + 4] = rb(hi[e]);
+    }
+  }
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
@@ -621,7 +630,18 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
     const int q = nwg / 8, r = nwg % 8, x = bid % 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
-  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  int tm, tn;
+  if (p.group_m > 1) {
+    // grouped order: an XCD's co-resident tiles form a group_m x (32 / group_m) block, so the
+    // A rows and B columns they read fit its L2 together (row-major order streams all of B)
+    const int span = p.group_m * p.tiles_n, g = bid / span, first = g * p.group_m;
+    const int gs = p.tiles_m - first < p.group_m ? p.tiles_m - first : p.group_m;
+    tm = first + (bid % span) % gs;
+    tn = (bid % span) / gs;
+  } else {
+    tm = bid / p.tiles_n;
+    tn = bid % p.tiles_n;
+  }
   const long m0 = (long)tm * 256, n0 = (long)tn * 256;
   const long z = blockIdx.z;
   const bf16* A = p.A + z * p.sA;
@@ -882,6 +902,10 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
   static const int pp = getenv("OWLK_GEMM_PP") ? atoi(getenv("OWLK_GEMM_PP")) : 1;
   static const int fuse_cs = getenv("OWLK_GEMM_COLSUM") ? atoi(getenv("OWLK_GEMM_COLSUM")) : 1;
   if (pp && EPI == EPI_DSILU && batch == 1 && fuse_cs) p.colsum = p.colsum_req;
+  // grouped tile order for the short-K GEMMs (K <= 2048: -2..4 % at dit_v4's K = 1536 shapes);
+  // at K >= 4608 and for split-K weight gradients row-major order measured equal or better
+  static const int group_m = getenv("OWLK_GEMM_GROUP") ? atoi(getenv("OWLK_GEMM_GROUP")) : -1;
+  p.group_m = group_m >= 0 ? group_m : (splits == 1 && p.kchunk <= 2048 ? 4 : 0);
   if (pp)
     hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   else
@@ -973,6 +997,174 @@ __global__ __launch_bounds__(256) void splitk_epi_k(GemmP p, int splits) {
   }
 }
 
+// ---------------------------------------------------------------- decode GEMM (M <= 128)
+// One 64-token frame (or a CFG pair of them) against full weight matrices: the weights are the
+// only large operand, so the kernel is a weight stream.  A workgroup owns 64 output columns over
+// all M rows (padded to MT) and one K chunk; its 4 waves take interleaved 32-deep K steps with
+// fragments loaded straight from global memory PD steps ahead (A re-read from L2, B streamed once)
+// and sum their partial tiles in LDS in wave order.  With several K chunks (gridDim.y) each
+// workgroup stores its fp32 partial tile and the last one to arrive at the tile (an arrival
+// counter) adds the partials in chunk order and applies the epilogue: one launch, deterministic.
+// ws = [tile counters: kDecodeCounterBytes, zero on entry and left zero][partials: S x tiles x MT x 64].
+constexpr int DEC_BN = 64;
+constexpr int DEC_LD = DEC_BN + 4;
+constexpr long kDecodeCounterBytes = 4096;
+
+template <int MT, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_decode_k(GemmP p, int* counters) {
+  constexpr int MI = MT / 16, NJ = DEC_BN / 16, PD = 4;
+  __shared__ __attribute__((aligned(16))) float red[4 * MT * DEC_LD];
+  __shared__ int ticket;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x, split = blockIdx.y, S = gridDim.y;
+  const long n0 = (long)tile * DEC_BN;
+  const long kbeg = (long)split * p.kchunk;
+  const long kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
+  const int nsteps = (int)((kend - kbeg) / 32);
+  const int nt = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;
+  const int r16 = lane & 15, k8 = 8 * (lane >> 4);
+  const bf16* arow[MI];
+  const bf16* brow[NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const long m = 16 * i + r16 < p.M ? 16 * i + r16 : p.M - 1;
+    arow[i] = p.A + m * p.lda + kbeg + k8;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) brow[j] = p.B + (n0 + 16 * j + r16) * p.ldb + kbeg + k8;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ra[PD][MI], rbq[PD][NJ];
+  // every load is issued unconditionally (past the wave's last step it re-reads the chunk's last
+  // step, unused): the loop then has a fixed load count per step and the compiler's waits are
+  // counted (vmcnt((PD - 1) x loads per step)) instead of draining all PD steps at once
+  auto load = [&](int d, int t) {
+    const int st = wave + 4 * t < nsteps ? wave + 4 * t : nsteps - 1;  // wave-local step t = chunk step wave + 4 t
+    const long k = 32L * st;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) ra[d][i] = *(const bf16x8*)(arow[i] + k);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) rbq[d][j] = *(const bf16x8*)(brow[j] + k);
+  };
+  auto mma = [&](int d) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[d][i], rbq[d][j], acc[i][j], 0, 0, 0);
+  };
+#pragma unroll
+  for (int d = 0; d < PD; ++d) load(d, d);
+  int t0 = 0;
+  for (; t0 + PD <= nt; t0 += PD) {  // branch-free body
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      mma(d);
+      load(d, t0 + d + PD);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < PD; ++d)  // the last (< PD) steps
+    if (t0 + d < nt) mma(d);
+  // wave partials -> LDS (C layout: lane holds column r16, rows 4 (lane >> 4) + r)
+  float* rw = red + wave * MT * DEC_LD;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rw[(16 * i + 4 * (lane >> 4) + r) * DEC_LD + 16 * j + r16] = acc[i][j][r];
+  __syncthreads();
+  float* part = p.ws + (long)tile * MT * DEC_BN;
+  const long pstride = (long)gridDim.x * MT * DEC_BN;  // between K chunks
+  for (int it = threadIdx.x; it < MT * (DEC_BN / 8); it += 256) {
+    const int row = it / (DEC_BN / 8), c = (it % (DEC_BN / 8)) * 8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const f32x4 lo = *(const f32x4*)(red + (w * MT + row) * DEC_LD + c);
+      const f32x4 hi = *(const f32x4*)(red + (w * MT + row) * DEC_LD + c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += lo[e];
+        v[e + 4] += hi[e];
+      }
+    }
+    if (S == 1) {
+      if (row < p.M) epi_chunk<EPI, false>(p, 0, row, n0 + c, v);
+    } else {
+      float* dst = part + split * pstride + row * DEC_BN + c;
+      *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+  if (S == 1) return;
+  // hand-off (cdna_hip_programming.md Guideline 16, counter form): every wave drains its partial
+  // stores, then ONE agent-scope release by lane 0 before the ticket (the reader may sit on another
+  // XCD); the last arriver's lane 0 acquires before anyone reads the other chunks' partials.  A
+  // __threadfence() in every thread instead costs ~3x the whole kernel.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int tk = __hip_atomic_fetch_add(counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == S - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    ticket = tk;
+  }
+  __syncthreads();
+  if (ticket != S - 1) return;
+  for (int it = threadIdx.x; it < MT * (DEC_BN / 8); it += 256) {
+    const int row = it / (DEC_BN / 8), c = (it % (DEC_BN / 8)) * 8;
+    if (row >= p.M) continue;
+    float v[8];
+    const float* src = part + row * DEC_BN + c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    for (int sp = 0; sp < S; ++sp) {
+      const f32x4 lo = *(const f32x4*)(src + sp * pstride), hi = *(const f32x4*)(src + sp * pstride + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += lo[e];
+        v[e + 4] += hi[e];
+      }
+    }
+    epi_chunk<EPI, false>(p, 0, row, n0 + c, v);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MT>
+int launch_decode_mt(GemmP& p, int epi, long tiles, long S, int* counters, hipStream_t s) {
+  const dim3 grid((unsigned)tiles, (unsigned)S);
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((gemm_decode_k<MT, EPI_STORE>), grid, dim3(256), 0, s, p, counters); break;
+    case EPI_SILU: hipLaunchKernelGGL((gemm_decode_k<MT, EPI_SILU>), grid, dim3(256), 0, s, p, counters); break;
+    default: hipLaunchKernelGGL((gemm_decode_k<MT, EPI_GATE_RESID>), grid, dim3(256), 0, s, p, counters); break;
+  }
+  return owlk::check_launch("gemm_decode");
+}
+
+int launch_decode(GemmP& p, int epi, long S, void* ws, hipStream_t s) {
+  const long tiles = p.N / DEC_BN;
+  int* counters = (int*)ws;
+  p.ws = S > 1 ? (float*)((char*)ws + kDecodeCounterBytes) : nullptr;
+  if (p.M <= 16) return launch_decode_mt<16>(p, epi, tiles, S, counters, s);
+  if (p.M <= 32) return launch_decode_mt<32>(p, epi, tiles, S, counters, s);
+  if (p.M <= 64) return launch_decode_mt<64>(p, epi, tiles, S, counters, s);
+  return launch_decode_mt<128>(p, epi, tiles, S, counters, s);
+}
+long decode_mt(long M) { return M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128; }
+
 // split-K factor for long reductions onto few 256^2 tiles (weight gradients, K = tokens): at one
 // workgroup per CU (128 KiB LDS) the grid runs in ceil(tiles * s / 256) rounds, so pick s to fill
 // the last round (e.g. 144 tiles: s = 4 -> 2.25 rounds, 75 % of the third idle; s = 7 -> 3.94);
@@ -1024,7 +1216,9 @@ static long skinny_splits(long M, long N, long K, long batch, int c_f32, int epi
 //   S256    fp32 weight gradients on 256^2 tiles: partials + splitk_reduce_k
 //   S128    fp32 long reductions that do not tile by 256 (e.g. proj_in dW, N = 128): 128^2 tiles,
 //           partials + splitk_reduce_k (fp32 atomics only without a workspace)
-enum SplitKind { SPLIT_NONE = 0, SPLIT_SKINNY, SPLIT_256, SPLIT_128 };
+//   DECODE  M <= 128 rows of bf16 output against k-contiguous weights (decode): gemm_decode_k,
+//           K chunks summed by the last workgroup of each 64-column tile
+enum SplitKind { SPLIT_NONE = 0, SPLIT_SKINNY, SPLIT_256, SPLIT_128, SPLIT_DECODE };
 struct SplitPlan {
   int kind;
   long splits, kchunk;
@@ -1033,6 +1227,20 @@ struct SplitPlan {
 static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta) {
   SplitPlan pl{SPLIT_NONE, 1, K};
+  static const int use_decode = getenv("OWLK_GEMM_DECODE") ? atoi(getenv("OWLK_GEMM_DECODE")) : 0;
+  if (use_decode && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_BN == 0 && K % 32 == 0 &&
+      N / DEC_BN <= kDecodeCounterBytes / 4 &&
+      (epi == EPI_SILU || epi == EPI_GATE_RESID || epi == EPI_STORE)) {
+    // K chunks (multiples of 4 waves x 32) so that ~256 workgroups stream the weights
+    const long tiles = N / DEC_BN;
+    long sp = (256 + tiles / 2) / tiles;
+    if (sp > K / 128) sp = K / 128;
+    if (sp < 1) sp = 1;
+    pl.kchunk = ((K + sp - 1) / sp + 127) / 128 * 128;
+    pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
+    pl.kind = SPLIT_DECODE;
+    return pl;
+  }
   auto chunk = [&](long sp) { return ((K + sp - 1) / sp + BK - 1) / BK * BK; };
   const long sk = skinny_splits(M, N, K, batch, c_f32, epi, beta);
   if (sk > 1) {
@@ -1070,6 +1278,8 @@ static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int
 // workspace bytes of a plan's per-split partials (0: the plan does not split or cannot use them)
 static long split_ws_bytes(const SplitPlan& pl, long M, long N, long batch) {
   if (pl.kind == SPLIT_NONE || (pl.kind == SPLIT_128 && batch != 1)) return 0;
+  if (pl.kind == SPLIT_DECODE)
+    return pl.splits > 1 ? kDecodeCounterBytes + pl.splits * decode_mt(M) * N * (long)sizeof(float) : 0;
   return pl.splits * M * N * (long)sizeof(float);
 }
 
@@ -1115,6 +1325,10 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
   const long pws = split_ws_bytes(pl, M, N, batch);
   const bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
+  if (pl.kind == SPLIT_DECODE && (pl.splits == 1 || have_ws)) {
+    p.kchunk = pl.kchunk;
+    return launch_decode(p, epi, pl.splits, ws, s);
+  }
   {
     const long sk = pl.splits;
     if (pl.kind == SPLIT_SKINNY && have_ws) {
@@ -1218,6 +1432,13 @@ extern "C" long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a
                                        int epi, float beta) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
   return split_ws_bytes(split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta), M, N, batch);
+}
+
+extern "C" long owlk_gemm_ws_counter_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32,
+                                           int epi, float beta) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0) return 0;
+  const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+  return pl.kind == SPLIT_DECODE && pl.splits > 1 ? kDecodeCounterBytes : 0;
 }
 
 extern "C" long owlk_gemm_ws_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,

@@ -19,6 +19,7 @@ _SIGS = {
                   P],
     "owlk_gemm_splitk_bytes": [L, L, L, L, I, I, I, I, F],
     "owlk_gemm_ws_bytes": [L, L, L, L, I, I, I, I, F, I],
+    "owlk_gemm_ws_counter_bytes": [L, L, L, L, I, I, I, I, F],
     "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
     "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
     "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],
@@ -53,8 +54,9 @@ _SIGS = {
 }
 
 # size queries; every other entry returns an int status
-_RESTYPES = {n: ctypes.c_long for n in ("owlk_gemm_splitk_bytes", "owlk_gemm_ws_bytes", "owlk_colsum_ws_bytes",
-                                        "owlk_ns_iterate_ws_bytes", "owlk_newton_schulz_ws_bytes")}
+_RESTYPES = {n: ctypes.c_long for n in ("owlk_gemm_splitk_bytes", "owlk_gemm_ws_bytes", "owlk_gemm_ws_counter_bytes",
+                                        "owlk_colsum_ws_bytes", "owlk_ns_iterate_ws_bytes",
+                                        "owlk_newton_schulz_ws_bytes")}
 
 _lib = None
 

@@ -51,11 +51,14 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
     # the deterministic form comes from torch's caching allocator (the library never allocates);
     # stream order keeps it alive for the launch
     ws, ws_bytes = None, 0
-    if (out_f32 and K >= 8192) or (M <= 256 and K >= 512 and not out_f32) or colsum is not None:
+    if (out_f32 and K >= 8192) or (M <= 256 and not out_f32) or colsum is not None:
         ws_bytes = lib().owlk_gemm_ws_bytes(M, N, K, 1, int(a_trans), int(b_trans), int(out_f32), epi, float(beta),
                                             int(colsum is not None))
         if ws_bytes > 0:
-            ws = torch.empty(ws_bytes, device=A.device, dtype=torch.uint8)
+            stateful = M <= 128 and not out_f32 and lib().owlk_gemm_ws_counter_bytes(
+                M, N, K, 1, int(a_trans), int(b_trans), int(out_f32), epi, float(beta)) > 0
+            ws = _decode_ws(A.device, ws_bytes) if stateful else \
+                torch.empty(ws_bytes, device=A.device, dtype=torch.uint8)
     call("owlk_gemm", M, N, K, 1,
          ptr(A), A.stride(0), 0, int(a_trans),
          ptr(B), B.stride(0), 0, int(b_trans),
@@ -67,6 +70,26 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
          ptr(colsum), ptr(ws), ws_bytes, stream(), key=f"gemm<{tile},{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
          flops=lambda: 2.0 * M * N * K)
     return out
+
+
+_DECODE_WS = {}
+
+
+def _decode_ws(device, nbytes):
+    """The decode GEMM plan's workspace (M <= 128 rows): its first 4 KiB are per-tile arrival
+    counters that must be zero on entry and that every launch leaves zero (owlk.h, owlk_gemm), so
+    one zero-initialised buffer is kept per device and reused; it grows by reallocation.  Decode
+    GEMMs therefore must not run concurrently on two streams of one device (the samplers issue them
+    on one stream, eagerly or by graph replay).  Under graph capture a too-small buffer is replaced
+    by a captured zero-fill of a fresh one."""
+    key = torch.device(device)
+    buf = _DECODE_WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        fresh = torch.zeros(max(nbytes, 1 << 20), device=device, dtype=torch.uint8)
+        if torch.cuda.is_current_stream_capturing():
+            return fresh
+        _DECODE_WS[key] = buf = fresh
+    return buf
 
 
 def gemm_wgrad(dy, x):

@@ -133,10 +133,16 @@ class DiTBlock(nn.Module):
         s = F.silu(cond)
         return self.adaln1.mod(s), self.gate1.mod(s), self.adaln2.mod(s), self.gate2.mod(s)
 
-    def forward(self, x, cond, block_mask, kv_cache=None):
+    def mod_params(self):
+        """(weights, biases) of the four per-frame modulation Linears, in the column order of
+        modulation()'s outputs: adaln1 [2d] | gate1 [d] | adaln2 [2d] | gate2 [d]."""
+        fcs = (self.adaln1.fc, self.gate1.fc_c, self.adaln2.fc, self.gate2.fc_c)
+        return [f.weight for f in fcs], [f.bias for f in fcs]
+
+    def forward(self, x, cond, block_mask, kv_cache=None, mods=None):
         if kv_cache is not None:
             with torch.no_grad():
-                return self._forward_cached(x, cond, block_mask, kv_cache)
+                return self._forward_cached(x, cond, block_mask, kv_cache, mods)
         cfg = self.config
         ab1, g1, ab2, g2 = self.modulation(cond)
         H = cfg.n_heads
@@ -147,11 +153,16 @@ class DiTBlock(nn.Module):
         return DiTBlockFn.apply(x.to(torch.bfloat16).contiguous(), ab1, g1, ab2, g2, a.qkv.weight, a.qkv.bias,
                                 a.out.weight, a.out.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias, geo)
 
-    def _forward_cached(self, x, cond, block_mask, kv_cache):
+    def _forward_cached(self, x, cond, block_mask, kv_cache, mods=None):
+        """No-grad forward of the decode path (attn.py:86-107 cache branch).  mods: this block's
+        [rows, 6d] column slice of DiT._decode_modulation, else computed here."""
         cfg = self.config
         d, tpf = cfg.d_model, cfg.tokens_per_frame
         B, L, _ = x.shape
-        ab1, g1, ab2, g2 = self.modulation(cond)
+        if mods is None:
+            ab1, g1, ab2, g2 = self.modulation(cond)
+        else:
+            ab1, g1, ab2, g2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
         xx = x.reshape(B * L, d).to(torch.bfloat16).contiguous()
         ab1, ab2 = ab1.reshape(-1, 2 * d), ab2.reshape(-1, 2 * d)
         h1, _ = K.adaln_fwd(xx, ab1[:, :d], ab1[:, d:], tpf)
@@ -200,12 +211,37 @@ class DiT(nn.Module):
         # optional: checkpoint only the first `checkpoint_layers` blocks and keep the rest's activations
         # (HBM headroom on a 288 GB MI355X trades for the recompute); default = every block, as the reference
         n_ck = getattr(self.config, "checkpoint_layers", None)
+        mods = self._decode_modulation(cond) if kv_cache is not None else None
+        d6 = 6 * self.config.d_model
         for i, block in enumerate(self.blocks):
             mask = local_block_mask if self.local_layers[i] else global_block_mask
+            if mods is not None:
+                x = block(x, cond, mask, kv_cache, mods[:, i * d6:(i + 1) * d6])
+                continue
             ck = ckpt and (n_ck is None or i < n_ck)
             block._checkpointed = ck  # the re-run inside backward reuses the kept attention output
             x = checkpoint(block, x, cond, mask, kv_cache) if ck else block(x, cond, mask, kv_cache)
         return x
+
+    @torch.no_grad()
+    def _decode_modulation(self, cond):
+        """Every block's per-frame modulation (DiTBlock.modulation) for a no-grad KV-cache forward
+        as ONE GEMM: silu(cond) [rows, d] against all blocks' modulation weights stacked
+        [L x 6d, d].  Decode has 1-2 rows per call, so the 4 x L per-block GEMMs were each a
+        latency-bound launch pair; the stacked GEMM streams the same 28 MB/block of weights once.
+        The bf16 stack is rebuilt when any of its parameters changes (version counters)."""
+        ws, bs = zip(*(b.mod_params() for b in self.blocks))
+        ws, bs = [w for g in ws for w in g], [b for g in bs for b in g]
+        key = (cond.device,) + tuple(p._version for p in ws + bs) + tuple(id(p) for p in ws)
+        ent = getattr(self, "_mod_stack", None)
+        if ent is None or ent[0] != key:
+            W = torch.cat([w.detach().to(torch.bfloat16) for w in ws]).contiguous()
+            bias = torch.cat([b.detach().float() for b in bs]).contiguous()
+            ent = (key, W, bias)
+            object.__setattr__(self, "_mod_stack", ent)
+        d = self.config.d_model
+        s = F.silu(cond.reshape(-1, d)).to(torch.bfloat16).contiguous()
+        return K.gemm(s, ent[1], bias=ent[2])
 
 
 class FinalLayer(nn.Module):

@@ -692,15 +692,18 @@ def test_fused_adamw_matches_torch(eps, wd):
     assert fo.state_dict()["param_groups"][0].keys() == to.state_dict()["param_groups"][0].keys()
 
 
-@pytest.mark.parametrize("M,N,Kd", [(64, 6144, 1536), (64, 1536, 6144), (128, 4608, 1536), (72, 256, 512)])
+@pytest.mark.parametrize("M,N,Kd", [(64, 6144, 1536), (64, 1536, 6144), (128, 4608, 1536), (72, 256, 512),
+                                    (1, 1536, 1536), (2, 3072, 128), (16, 256, 64), (40, 1536, 4608),
+                                    (200, 1536, 1536)])
 def test_gemm_skinny_splitk_epilogues(M, N, Kd):
-    """Skinny-M GEMMs (decode: one 64-token frame) split K over the workspace and apply the epilogue
-    after a fixed-order reduce: store + bias, SiLU + aux, gate + residual vs fp32 torch (bf16 output
-    tolerance 5e-3), deterministic across runs, and the same numbers as the unsplit path up to fp32
-    summation order."""
+    """Skinny-M GEMMs (decode: one 64-token frame, a CFG pair, per-frame rows).  M <= 128 takes the
+    one-launch decode plan (K chunks summed in order by each tile's last workgroup, arrival counters
+    left zero), 128 < M <= 256 the split-K partials + reduce kernel.  Store + bias, SiLU + aux,
+    gate + residual vs fp32 torch (bf16 output tolerance 5e-3), deterministic across runs."""
     k = K()
     from owl_wms._lib import lib
-    assert lib().owlk_gemm_splitk_bytes(M, N, Kd, 1, 0, 0, 0, k.EPI_SILU, 0.0) > 0  # the split path is taken
+    if Kd >= 512:  # the split path is taken
+        assert lib().owlk_gemm_splitk_bytes(M, N, Kd, 1, 0, 0, 0, k.EPI_SILU, 0.0) > 0
     tpf = 64 if M % 64 == 0 else M
     A, W = rnd(M, Kd, seed=13), rnd(N, Kd, scale=0.05, seed=14)
     bias = (torch.randn(N) * 0.1).to(DEV)
@@ -717,6 +720,11 @@ def test_gemm_skinny_splitk_epilogues(M, N, Kd):
     o = k.gemm(A, W, bias=bias, epi=k.EPI_GATE_RESID, gate=g, tpf=tpf, resid=res)
     gref = g.float().repeat_interleave(tpf, 0)[:M]
     assert rel(o, res.float() + gref * y) < 5e-3
+    c0 = rnd(M, N, seed=17)
+    c1 = k.gemm(A, W, out=c0.clone(), alpha=0.5, beta=1.0)  # STORE with beta: C read back
+    assert rel(c1, 0.5 * acc + c0.float()) < 5e-3
+    for ws in k._DECODE_WS.values():  # every launch left its arrival counters at zero
+        assert int(ws[:4096].count_nonzero()) == 0
 
 
 @pytest.mark.parametrize("case", [(2, 2, 12, 64, None), (1, 2, 24, 64, 16), (2, 1, 9, 4, 3), (1, 2, 7, 65, None),
