@@ -102,7 +102,8 @@ def cpu_baseline(steps=3):
                       f"sequence than the GPU workload"}
 
 
-PMC_KERNELS = {"attn_bwd_dkdv": "attn_bwd_dkdv_k", "attn_bwd_dq": "attn_bwd_dq_k", "attn_fwd": "attn_fwd"}
+# kernel symbols (the 16x16x32 and 32x32x16 variants of each)
+PMC_KERNELS = {"attn_bwd_dkdv": "attn_bwd_dkdv(16)?_k", "attn_bwd_dq": "attn_bwd_dq(16)?_k", "attn_fwd": "attn_fwd"}
 
 
 def pmc_traffic(args):
