@@ -998,172 +998,181 @@ __global__ __launch_bounds__(256) void splitk_epi_k(GemmP p, int splits) {
 }
 
 // ---------------------------------------------------------------- decode GEMM (M <= 128)
-// One 64-token frame (or a CFG pair of them) against full weight matrices: the weights are the
-// only large operand, so the kernel is a weight stream.  A workgroup owns 64 output columns over
-// all M rows (padded to MT) and one K chunk; its 4 waves take interleaved 32-deep K steps with
-// fragments loaded straight from global memory PD steps ahead (A re-read from L2, B streamed once)
-// and sum their partial tiles in LDS in wave order.  With several K chunks (gridDim.y) each
-// workgroup stores its fp32 partial tile and the last one to arrive at the tile (an arrival
-// counter) adds the partials in chunk order and applies the epilogue: one launch, deterministic.
-// ws = [tile counters: kDecodeCounterBytes, zero on entry and left zero][partials: S x tiles x MT x 64].
-constexpr int DEC_BN = 64;
-constexpr int DEC_LD = DEC_BN + 4;
+// One 64-token frame (or a CFG pair of them) against full weight matrices: a weight stream.  A
+// workgroup owns a 64-row x 64-column output tile and one K chunk of nsub x 256: per 256-deep
+// sub-chunk its 4 waves stage the 64 weight rows and 64 activation rows into LDS by LDS-DMA in
+// whole 512-B rows (full cache lines; fragment-shaped global loads were TA-bound), then each wave
+// multiplies its 16 activation rows against all 64 columns from LDS.  With several K chunks
+// (gridDim.y) each workgroup stores its fp32 partial tile and the last one to arrive at the tile
+// (arrival counter, agent-scope release/acquire) adds the partials in chunk order and applies the
+// epilogue: one launch, deterministic.
+// ws = [tile counters: kDecodeCounterBytes, zero on entry, left zero][partials: S x M_pad x N fp32].
+constexpr int DEC_T = 64;              // tile rows = tile columns
+constexpr int DEC_KC = 256;            // K per staged sub-chunk
+constexpr int DEC_ROWB = DEC_KC * 2;   // bytes per staged row
+constexpr int DEC_LD = DEC_T + 4;      // fp32 output tile row stride (floats)
 constexpr long kDecodeCounterBytes = 4096;
 
-template <int MT, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_decode_k(GemmP p, int* counters) {
-  constexpr int MI = MT / 16, NJ = DEC_BN / 16, PD = 4;
-  __shared__ __attribute__((aligned(16))) float red[4 * MT * DEC_LD];
-  __shared__ int ticket;
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_decode_k(GemmP p, int* counters, int nsub) {
+  // two stages of [W rows 0-63 | X rows 64-127] x 512 B, 16-B chunks XOR-swizzled by (row & 31)
+  // (conflict-free fragment reads); afterwards stage 0 holds the fp32 tile and the last-arriver
+  // flag (one __shared__ object)
+  constexpr int STAGE = 2 * DEC_T * DEC_ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  float* tilef = (float*)smem;
+  int* flag = (int*)(smem + DEC_T * DEC_LD * 4);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x, split = blockIdx.y, S = gridDim.y;
-  const long n0 = (long)tile * DEC_BN;
-  const long kbeg = (long)split * p.kchunk;
-  const long kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
-  const int nsteps = (int)((kend - kbeg) / 32);
-  const int nt = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;
-  const int r16 = lane & 15, k8 = 8 * (lane >> 4);
-  const bf16* arow[MI];
-  const bf16* brow[NJ];
+  const int tile = blockIdx.x, split = blockIdx.y, S = gridDim.y, mt = blockIdx.z;
+  const int tiles = gridDim.x;
+  const long n0 = (long)tile * DEC_T, m0 = (long)mt * DEC_T;
+  const int r16 = lane & 15, g = lane >> 4;
+  const long kfirst = (long)split * nsub * DEC_KC;
+  const int nst = (int)((p.K - kfirst + DEC_KC - 1) / DEC_KC < nsub ? (p.K - kfirst + DEC_KC - 1) / DEC_KC : nsub);
+  // stage i: waves 0-1 move the 64 weight rows, waves 2-3 the 64 activation rows; a
+  // wave-instruction moves 2 rows x 32 chunks (lane -> row + (lane >> 5), LDS slot lane & 31)
+  const bool isw = wave < 2;
+  const bf16* rowp[16];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const long m = 16 * i + r16 < p.M ? 16 * i + r16 : p.M - 1;
-    arow[i] = p.A + m * p.lda + kbeg + k8;
-  }
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) brow[j] = p.B + (n0 + 16 * j + r16) * p.ldb + kbeg + k8;
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ra[PD][MI], rbq[PD][NJ];
-  // every load is issued unconditionally (past the wave's last step it re-reads the chunk's last
-  // step, unused): the loop then has a fixed load count per step and the compiler's waits are
-  // counted (vmcnt((PD - 1) x loads per step)) instead of draining all PD steps at once
-  auto load = [&](int d, int t) {
-    const int st = wave + 4 * t < nsteps ? wave + 4 * t : nsteps - 1;  // wave-local step t = chunk step wave + 4 t
-    const long k = 32L * st;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) ra[d][i] = *(const bf16x8*)(arow[i] + k);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) rbq[d][j] = *(const bf16x8*)(brow[j] + k);
-  };
-  auto mma = [&](int d) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[d][i], rbq[d][j], acc[i][j], 0, 0, 0);
-  };
-#pragma unroll
-  for (int d = 0; d < PD; ++d) load(d, d);
-  int t0 = 0;
-  for (; t0 + PD <= nt; t0 += PD) {  // branch-free body
-#pragma unroll
-    for (int d = 0; d < PD; ++d) {
-      mma(d);
-      load(d, t0 + d + PD);
+  for (int j = 0; j < 16; ++j) {
+    const int r = (wave & 1) * 32 + 2 * j + (lane >> 5);
+    if (isw) {
+      rowp[j] = p.B + (n0 + r) * p.ldb;
+    } else {
+      const long m = m0 + r < p.M ? m0 + r : p.M - 1;
+      rowp[j] = p.A + m * p.lda;
     }
   }
+  const int ldsrow0 = (isw ? 0 : DEC_T) + (wave & 1) * 32;
+  auto issue = [&](int i) {
+    const long kbeg = kfirst + (long)i * DEC_KC;
+    const int nch = (int)((p.K - kbeg < DEC_KC ? p.K - kbeg : DEC_KC) / 8);
+    char* buf = smem + (i & 1) * STAGE + ldsrow0 * DEC_ROWB;
 #pragma unroll
-  for (int d = 0; d < PD; ++d)  // the last (< PD) steps
-    if (t0 + d < nt) mma(d);
-  // wave partials -> LDS (C layout: lane holds column r16, rows 4 (lane >> 4) + r)
-  float* rw = red + wave * MT * DEC_LD;
+    for (int j = 0; j < 16; ++j) {
+      const int r = 2 * j + (lane >> 5);
+      int ch = (lane & 31) ^ r;  // (staged row & 31) == r
+      ch = ch < nch ? ch : nch - 1;  // past a short last chunk: a valid address, never read
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(rowp[j] + kbeg + ch * 8),
+                                       (void __attribute__((address_space(3)))*)(buf + 2 * j * DEC_ROWB), 16, 0, 0);
+    }
+  };
+  f32x4 acc[4];
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int xr = DEC_T + 16 * wave + r16;  // this lane's staged activation row
+  issue(0);
+  if (nst > 1) issue(1);
+  for (int sc = 0; sc < nst; ++sc) {
+    // raw barriers: __syncthreads() would make hipcc drain the next stage's DMA (vmcnt(0)) too
+    if (sc + 1 < nst)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // stage sc landed, sc + 1 still in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    const long kbeg = kfirst + (long)sc * DEC_KC;
+    const int kc = (int)(p.K - kbeg < DEC_KC ? p.K - kbeg : DEC_KC);  // multiple of 32
+    const char* buf = smem + (sc & 1) * STAGE;
+    for (int st = 0; st < kc / 32; ++st) {
+      const int c = 4 * st + g;
+      const bf16x8 a = *(const bf16x8*)(buf + xr * DEC_ROWB + ((c ^ (xr & 31)) << 4));
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rw[(16 * i + 4 * (lane >> 4) + r) * DEC_LD + 16 * j + r16] = acc[i][j][r];
-  __syncthreads();
-  float* part = p.ws + (long)tile * MT * DEC_BN;
-  const long pstride = (long)gridDim.x * MT * DEC_BN;  // between K chunks
-  for (int it = threadIdx.x; it < MT * (DEC_BN / 8); it += 256) {
-    const int row = it / (DEC_BN / 8), c = (it % (DEC_BN / 8)) * 8;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const f32x4 lo = *(const f32x4*)(red + (w * MT + row) * DEC_LD + c);
-      const f32x4 hi = *(const f32x4*)(red + (w * MT + row) * DEC_LD + c + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] += lo[e];
-        v[e + 4] += hi[e];
+      for (int j = 0; j < 4; ++j) {
+        const int wr = 16 * j + r16;
+        const bf16x8 b = *(const bf16x8*)(buf + wr * DEC_ROWB + ((c ^ (wr & 31)) << 4));
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
       }
     }
+    if (sc + 2 < nst) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done reading it
+      issue(sc + 2);
+    }
+  }
+  __syncthreads();  // staging reads done: the LDS now takes the fp32 tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tilef[(16 * wave + 4 * g + r) * DEC_LD + 16 * j + r16] = acc[j][r];
+  __syncthreads();
+  const long rows = p.M - m0 < DEC_T ? p.M - m0 : DEC_T;
+  // partials [mt][split][tile][64 x 64] fp32 through a buffer descriptor (byte offsets < 2^31)
+  const long pstride = (long)tiles * DEC_T * DEC_T * 4;  // bytes between K chunks
+  const long mbase = (long)mt * S * pstride + (long)tile * DEC_T * DEC_T * 4;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(p.ws, (short)0, S > 1 ? (int)(S * pstride * gridDim.z) : 0, 0x00020000);
+  for (int it = threadIdx.x; it < DEC_T * (DEC_T / 8); it += 256) {
+    const int row = it >> 3, c = (it & 7) * 8;
+    if (row >= rows) continue;
+    const f32x4 lo = *(const f32x4*)(tilef + row * DEC_LD + c), hi = *(const f32x4*)(tilef + row * DEC_LD + c + 4);
     if (S == 1) {
-      if (row < p.M) epi_chunk<EPI, false>(p, 0, row, n0 + c, v);
-    } else {
-      float* dst = part + split * pstride + row * DEC_BN + c;
-      *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
-      *(f32x4*)(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      epi_chunk<EPI, false>(p, 0, m0 + row, n0 + c, v);
+    } else {  // write-through (sc1) stores: visible to any XCD without a release fence
+      const int off = (int)(mbase + split * pstride + (row * DEC_T + c) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), prs, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), prs, off + 16, 0, 16);
     }
   }
   if (S == 1) return;
-  // hand-off (cdna_hip_programming.md Guideline 16, counter form): every wave drains its partial
-  // stores, then ONE agent-scope release by lane 0 before the ticket (the reader may sit on another
-  // XCD); the last arriver's lane 0 acquires before anyone reads the other chunks' partials.  A
-  // __threadfence() in every thread instead costs ~3x the whole kernel.
+  // hand-off (cdna_hip_programming.md Guideline 16, R1 with a counter): every wave drains its sc1
+  // partial stores, then lane 0 adds to the tile's arrival counter; the last arriver reads every
+  // partial with sc1 loads (past this CU's L1), so neither side needs an agent fence.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int tk = __hip_atomic_fetch_add(counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == S - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    ticket = tk;
-  }
+  int* cnt = counters + mt * tiles + tile;
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (ticket != S - 1) return;
-  for (int it = threadIdx.x; it < MT * (DEC_BN / 8); it += 256) {
-    const int row = it / (DEC_BN / 8), c = (it % (DEC_BN / 8)) * 8;
-    if (row >= p.M) continue;
+  if (*flag != S - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  for (int it = threadIdx.x; it < DEC_T * (DEC_T / 8); it += 256) {
+    const int row = it >> 3, c = (it & 7) * 8;
+    if (row >= rows) continue;
+    const int off = (int)(mbase + (row * DEC_T + c) * 4);
     float v[8];
-    const float* src = part + row * DEC_BN + c;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll 4
     for (int sp = 0; sp < S; ++sp) {
-      const f32x4 lo = *(const f32x4*)(src + sp * pstride), hi = *(const f32x4*)(src + sp * pstride + 4);
+      const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, off + sp * (int)pstride, 0, 16));
+      const f32x4 hi =
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, off + sp * (int)pstride + 16, 0, 16));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[e] += lo[e];
         v[e + 4] += hi[e];
       }
     }
-    epi_chunk<EPI, false>(p, 0, row, n0 + c, v);
+    epi_chunk<EPI, false>(p, 0, m0 + row, n0 + c, v);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int MT>
-int launch_decode_mt(GemmP& p, int epi, long tiles, long S, int* counters, hipStream_t s) {
-  const dim3 grid((unsigned)tiles, (unsigned)S);
+// (K chunks, sub-chunks per chunk) of the decode plan
+void decode_split(long M, long N, long K, long& S, long& nsub) {
+  const long mtiles = (M + DEC_T - 1) / DEC_T, tiles = N / DEC_T, subs = (K + DEC_KC - 1) / DEC_KC;
+  // one workgroup per CU (128 KiB of LDS): split K only as far as it fills the 256 CUs
+  static const int force = getenv("OWLK_DECODE_NSUB") ? atoi(getenv("OWLK_DECODE_NSUB")) : 0;
+  long sp = 256 / (tiles * mtiles);
+  if (sp < 1) sp = 1;
+  nsub = force > 0 ? force : (subs + sp - 1) / sp;
+  if (nsub > subs) nsub = subs;
+  S = (subs + nsub - 1) / nsub;
+}
+
+int launch_decode(GemmP& p, int epi, void* ws, hipStream_t s) {
+  long S, nsub;
+  decode_split(p.M, p.N, p.K, S, nsub);
+  const long tiles = p.N / DEC_T, mtiles = (p.M + DEC_T - 1) / DEC_T;
+  int* counters = (int*)ws;
+  p.ws = S > 1 ? (float*)((char*)ws + kDecodeCounterBytes) : nullptr;
+  const dim3 grid((unsigned)tiles, (unsigned)S, (unsigned)mtiles);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_decode_k<MT, EPI_STORE>), grid, dim3(256), 0, s, p, counters); break;
-    case EPI_SILU: hipLaunchKernelGGL((gemm_decode_k<MT, EPI_SILU>), grid, dim3(256), 0, s, p, counters); break;
-    default: hipLaunchKernelGGL((gemm_decode_k<MT, EPI_GATE_RESID>), grid, dim3(256), 0, s, p, counters); break;
+    case EPI_STORE: hipLaunchKernelGGL(gemm_decode_k<EPI_STORE>, grid, dim3(256), 0, s, p, counters, (int)nsub); break;
+    case EPI_SILU: hipLaunchKernelGGL(gemm_decode_k<EPI_SILU>, grid, dim3(256), 0, s, p, counters, (int)nsub); break;
+    default: hipLaunchKernelGGL(gemm_decode_k<EPI_GATE_RESID>, grid, dim3(256), 0, s, p, counters, (int)nsub); break;
   }
   return owlk::check_launch("gemm_decode");
 }
-
-int launch_decode(GemmP& p, int epi, long S, void* ws, hipStream_t s) {
-  const long tiles = p.N / DEC_BN;
-  int* counters = (int*)ws;
-  p.ws = S > 1 ? (float*)((char*)ws + kDecodeCounterBytes) : nullptr;
-  if (p.M <= 16) return launch_decode_mt<16>(p, epi, tiles, S, counters, s);
-  if (p.M <= 32) return launch_decode_mt<32>(p, epi, tiles, S, counters, s);
-  if (p.M <= 64) return launch_decode_mt<64>(p, epi, tiles, S, counters, s);
-  return launch_decode_mt<128>(p, epi, tiles, S, counters, s);
-}
-long decode_mt(long M) { return M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128; }
 
 // split-K factor for long reductions onto few 256^2 tiles (weight gradients, K = tokens): at one
 // workgroup per CU (128 KiB LDS) the grid runs in ceil(tiles * s / 256) rounds, so pick s to fill
@@ -1227,17 +1236,11 @@ struct SplitPlan {
 static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta) {
   SplitPlan pl{SPLIT_NONE, 1, K};
-  static const int use_decode = getenv("OWLK_GEMM_DECODE") ? atoi(getenv("OWLK_GEMM_DECODE")) : 0;
-  if (use_decode && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_BN == 0 && K % 32 == 0 &&
-      N / DEC_BN <= kDecodeCounterBytes / 4 &&
+  static const int use_decode = getenv("OWLK_GEMM_DECODE") ? atoi(getenv("OWLK_GEMM_DECODE")) : 1;
+  if (use_decode && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_T == 0 && K % 32 == 0 &&
+      ((M + DEC_T - 1) / DEC_T) * (N / DEC_T) <= kDecodeCounterBytes / 4 &&
       (epi == EPI_SILU || epi == EPI_GATE_RESID || epi == EPI_STORE)) {
-    // K chunks (multiples of 4 waves x 32) so that ~256 workgroups stream the weights
-    const long tiles = N / DEC_BN;
-    long sp = (256 + tiles / 2) / tiles;
-    if (sp > K / 128) sp = K / 128;
-    if (sp < 1) sp = 1;
-    pl.kchunk = ((K + sp - 1) / sp + 127) / 128 * 128;
-    pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
+    decode_split(M, N, K, pl.splits, pl.kchunk);  // kchunk field: sub-chunks per chunk
     pl.kind = SPLIT_DECODE;
     return pl;
   }
@@ -1279,7 +1282,8 @@ static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int
 static long split_ws_bytes(const SplitPlan& pl, long M, long N, long batch) {
   if (pl.kind == SPLIT_NONE || (pl.kind == SPLIT_128 && batch != 1)) return 0;
   if (pl.kind == SPLIT_DECODE)
-    return pl.splits > 1 ? kDecodeCounterBytes + pl.splits * decode_mt(M) * N * (long)sizeof(float) : 0;
+    return pl.splits > 1 ? kDecodeCounterBytes + pl.splits * ((M + DEC_T - 1) / DEC_T) * DEC_T * N * (long)sizeof(float)
+                         : 0;
   return pl.splits * M * N * (long)sizeof(float);
 }
 
@@ -1325,10 +1329,7 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
   const long pws = split_ws_bytes(pl, M, N, batch);
   const bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
-  if (pl.kind == SPLIT_DECODE && (pl.splits == 1 || have_ws)) {
-    p.kchunk = pl.kchunk;
-    return launch_decode(p, epi, pl.splits, ws, s);
-  }
+  if (pl.kind == SPLIT_DECODE && (pl.splits == 1 || have_ws)) return launch_decode(p, epi, ws, s);
   {
     const long sk = pl.splits;
     if (pl.kind == SPLIT_SKINNY && have_ws) {

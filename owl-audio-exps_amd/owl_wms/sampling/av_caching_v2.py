@@ -47,18 +47,22 @@ class AVCachingSamplerV2:
             pred_v = model(x, t, mouse, btn, kv_cache=kv_cache)
         return x - dt * pred_v, t - dt
 
-    def _euler_graphed(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
-        """The frame's n_steps Euler steps with steps 1.. replayed from one HIP graph.
+    def _euler_graphed(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt, warm=True):
+        """The frame's n_steps Euler steps replayed from one HIP graph.
 
         The cache is read-only and fixed in length while a frame is denoised, so every step launches
-        the same kernels on the same buffers: step 0 runs eagerly (it also warms the per-weight bf16
-        caches), one step is captured with x, t and dt in static device buffers, and the graph is
-        replayed for the remaining steps -- same kernels and arithmetic as the eager loop
-        (the reference's ``compile_on_decode`` switch)."""
-        x, t = self._euler_step(model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt[0])
-        if self.n_steps == 1:
-            return x, t
-        sx, st, sdt = x.clone(), t.clone(), dt[1].clone()
+        the same kernels on the same buffers: one step is captured with x, t and dt in static device
+        buffers and replayed -- same kernels and arithmetic as the eager loop (the reference's
+        ``compile_on_decode`` switch).  With ``warm`` (the first frame) step 0
+        runs eagerly first: it creates the per-weight bf16 copies and workspaces outside the graph's
+        memory pool; later frames replay every step."""
+        first = 0
+        if warm:
+            x, t = self._euler_step(model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt[0])
+            first = 1
+            if self.n_steps == 1:
+                return x, t
+        sx, st, sdt = x.clone(), t.clone(), dt[first].clone()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
@@ -70,7 +74,7 @@ class AVCachingSamplerV2:
                 sx.copy_(nx)
                 st.copy_(nt)
         torch.cuda.current_stream().wait_stream(side)
-        for t_idx in range(1, self.n_steps):
+        for t_idx in range(first, self.n_steps):
             sdt.copy_(dt[t_idx])
             g.replay()
         del g
@@ -110,7 +114,7 @@ class AVCachingSamplerV2:
                 null_mouse, null_btn = torch.zeros_like(curr_mouse), torch.zeros_like(curr_btn)
                 if compile_on_decode:
                     curr_x, curr_t = self._euler_graphed(model, kv_cache, curr_x, curr_t, curr_mouse, curr_btn,
-                                                         null_mouse, null_btn, dt)
+                                                         null_mouse, null_btn, dt, warm=idx == 0)
                 else:
                     for t_idx in range(self.n_steps):
                         curr_x, curr_t = self._euler_step(model, kv_cache, curr_x, curr_t, curr_mouse, curr_btn,

@@ -14,17 +14,29 @@ import torch  # noqa: E402
 from owl_wms import kernels as K  # noqa: E402
 
 
-def timeit(fn, iters=200):
-    for _ in range(5):
-        fn()
+def timeit(fn, iters=50, reps=10):
+    """GPU time per call: the calls are captured into a HIP graph and replayed (a Python loop of
+    launches is CPU-bound at these sizes, ~14 us per call)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(reps):
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / iters * 1e3  # us
+    return e0.elapsed_time(e1) / (iters * reps) * 1e3  # us
 
 
 def main():
