@@ -700,10 +700,182 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   }
 }
 
+// Decode form of attn_fwd16_k (D = 64, bounded softmax, no mask: one new frame of Lq <= 64 queries
+// against [cache | frame]).  A (batch, head) has a single 64-query block, so attn_fwd16_k would run
+// one wave per workgroup over every key tile in turn.  Here the 4 waves share the queries and split
+// the key tiles (wave w takes tiles w, w + 4, ...), each streaming its tiles by LDS-DMA into a
+// private 2-slot ring (no barriers in the sweep); with the bounded softmax (no running maximum)
+// the waves' partial O and row sums simply add, in wave order, through LDS at the end.
+__global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p) {
+  using C = Cfg<64>;
+  constexpr int RING = 2 * C::TILEB;  // per wave
+  constexpr int OLD = 68;             // fp32 row stride of the combine image
+  __shared__ __attribute__((aligned(16))) char smem[4 * RING];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const long b = blockIdx.z;
+  const int head = blockIdx.y;
+  const bf16* Q = p.q + b * p.sqb + head * 64;
+  const bf16* K = p.k + b * p.skb + head * 64;
+  const bf16* V = p.v + b * p.svb + head * 64;
+  const int ntiles = (int)((p.Lkv + KT - 1) / KT);
+  const int nt = ntiles > w ? (ntiles - w + 3) / 4 : 0;  // this wave's tiles: w + 4 i
+
+  int my_q[4];
+  bf16x8 qf[4][2];
+#pragma unroll
+  for (int t4 = 0; t4 < 4; ++t4) {
+    my_q[t4] = 16 * t4 + c;
+#pragma unroll
+    for (int kd = 0; kd < 2; ++kd) {
+      bf16x8 qv = my_q[t4] < p.Lq ? *(const bf16x8*)(Q + my_q[t4] * p.ldq + 32 * kd + 8 * g) : bf16x8{};
+      float f[8];
+      unpack8(qv, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= p.scale_log2;
+      qf[t4][kd] = pack8(f);
+    }
+  }
+  f32x4 o[4][4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) o[ds][t4] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float lrow[4] = {0.f, 0.f, 0.f, 0.f};
+
+  char* ring = smem + w * RING;
+  auto issue = [&](int i) {  // the wave's i-th tile (key tile w + 4 i), all 64 rows by this wave
+    const long c0 = (long)(w + 4 * i) * KT;
+    char* buf = ring + (i & 1) * C::TILEB;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      tile_glds<SW_ROW>(buf, K, p.ldk, c0, p.Lkv, q4, lane);
+      tile_glds<SW_TR>(buf + SUB, V, p.ldv, c0, p.Lkv, q4, lane);
+    }
+  };
+  if (nt > 0) issue(0);
+  if (nt > 1) issue(1);
+  for (int i = 0; i < nt; ++i) {
+    if (i + 1 < nt)
+      vmcnt<16>();  // tile i landed (this wave's own DMA: no barrier), i + 1 in flight
+    else
+      vmcnt<0>();
+    const long c0 = (long)(w + 4 * i) * KT;
+    const char* lk = ring + (i & 1) * C::TILEB;
+    const char* lv = lk + SUB;
+    const bool ragged = c0 + KT > p.Lkv;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      f32x4 st[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) st[kk][t4] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kd = 0; kd < 2; ++kd)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 ak = frag_row16<SW_ROW>(lk, 32 * kc + 16 * kk, kd, lane);
+#pragma unroll
+          for (int t4 = 0; t4 < 4; ++t4)
+            st[kk][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t4][kd], st[kk][t4], 0, 0, 0);
+        }
+      if (ragged) {
+        __asm__ volatile("");  // keep the uniform branch a branch
+        const long kb0 = c0 + 32 * kc + 4 * g;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kb0 + 16 * kk + r >= p.Lkv)
+#pragma unroll
+              for (int t4 = 0; t4 < 4; ++t4) st[kk][t4][r] = -INFINITY;
+      }
+      bf16x8 pf[4];
+#pragma unroll
+      for (int t4 = 0; t4 < 4; ++t4) {
+        float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(st[kk][t4][r]);
+            st[kk][t4][r] = pv;
+            if (r & 1)
+              ps1 += pv;
+            else
+              ps0 += pv;
+          }
+        lrow[t4] += ps0 + ps1;
+        pf[t4] = pack_perm(st[0][t4], st[1][t4]);
+      }
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        const bf16x8 vt = frag_tr16<SW_TR>(lv, 32 * kc, ds, lane);
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4)
+          o[ds][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pf[t4], o[ds][t4], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (i + 2 < nt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's reads retired before its refill
+      issue(i + 2);
+    }
+  }
+  // combine: wave partials (O^T tiles: d = 16 ds + 4 g + r, query 16 t4 + c) -> LDS [w][q][d], then
+  // each thread sums one query's 16 columns over the 4 waves in order
+  vmcnt<0>();
+  __syncthreads();
+  float* img = (float*)smem;                      // [4][64][OLD]
+  float* lsum = (float*)(smem + 4 * 64 * OLD * 4);  // [4][64]
+#pragma unroll
+  for (int t4 = 0; t4 < 4; ++t4) {
+    const int q = 16 * t4 + c;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) img[(w * 64 + q) * OLD + 16 * ds + 4 * g + r] = o[ds][t4][r];
+    float lt = lrow[t4] + __shfl_xor(lrow[t4], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (g == 0) lsum[w * 64 + q] = lt;
+  }
+  __syncthreads();
+  const int q = threadIdx.x >> 2, d0 = 16 * (threadIdx.x & 3);
+  if (q >= p.Lq) return;
+  float l = 0.f;
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) l += lsum[ww * 64 + q];
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  bf16* O = p.o + b * p.sob + (long)q * p.ldo + head * 64 + d0;
+#pragma unroll
+  for (int h8 = 0; h8 < 2; ++h8) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += img[(ww * 64 + q) * OLD + d0 + 8 * h8 + e];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= inv;
+    *(bf16x8*)(O + 8 * h8) = pack8(v);
+  }
+  if ((threadIdx.x & 3) == 0) p.lse[(b * p.H + head) * p.Lq + q] = l > 0.f ? __log2f(l) : -INFINITY;
+}
+
 template <int D>
 void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   static const int two = getenv("OWLK_FWD2") ? atoi(getenv("OWLK_FWD2")) : 1;
   static const int f16 = getenv("OWLK_FWD16") ? atoi(getenv("OWLK_FWD16")) : 1;  // 16x16x32 variant (0: off)
+  // decode: one unmasked <= 64-query block per (batch, head) over >= 4 key tiles
+  static const int split = getenv("OWLK_FWD_SPLIT") ? atoi(getenv("OWLK_FWD_SPLIT")) : 1;
+  const MaskP& m = p.m;
+  if (D == 64 && split && p.bound > 0.f && p.Lq <= 64 && p.Lkv >= 4 * KT && m.window == 0 && !m.causal &&
+      !m.kv_lo && !m.doc && m.q_offset == 0) {
+    hipLaunchKernelGGL(attn_fwd16_split_k, dim3(1, grid.y, grid.z), dim3(256), 0, s, p);
+    return;
+  }
   if (D == 64 && f16 && p.bound > 0.f) {
     const dim3 g2((unsigned)((p.Lq + QT2 - 1) / QT2), grid.y, grid.z);
     hipLaunchKernelGGL((attn_fwd16_k<true>), g2, dim3(256), 0, s, p);

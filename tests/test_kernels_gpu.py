@@ -281,6 +281,31 @@ def test_attention_fwd_score_bound(case, D):
     assert rel(o, o0) < 5e-3
 
 
+@pytest.mark.parametrize("Lq,Lkv", [(64, 256), (64, 640), (37, 1000), (64, 4096), (1, 320)])
+def test_attention_decode_split_keys(Lq, Lkv):
+    """Decode attention (one frame of <= 64 queries, unmasked over [cache | frame], bounded
+    softmax): the 4 waves of a workgroup split the key tiles and add their partial O / row sums.
+    == oracle (rel 1e-2); lse within 4e-3 of the single-wave kernel (OWLK_FWD_SPLIT=0 path is the
+    one every other test covers); deterministic."""
+    k = K()
+    B, H, D = 2, 3, 64
+    unit = lambda t, L: (t.float().view(-1, H, D) * torch.rsqrt(t.float().view(-1, H, D).pow(2).mean(-1, keepdim=True))
+                         ).bfloat16().view(B, L, H * D)
+    q = unit(rnd(B * Lq, H * D, seed=70), Lq)
+    kk = unit(rnd(B * Lkv, H * D, seed=71), Lkv)
+    v = rnd(B * Lkv, H * D, seed=72).view(B, Lkv, H * D)
+    mask = k.FrameMask(1, None, False, 0, None)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask, score_bound=k.qk_norm_bound(D))
+    ref = R.attention(q.cpu().float().view(B, Lq, H, D).transpose(1, 2), kk.cpu().float().view(B, Lkv, H, D).transpose(1, 2),
+                      v.cpu().float().view(B, Lkv, H, D).transpose(1, 2))
+    assert rel(o.view(B, Lq, H, D).transpose(1, 2), ref) < 1e-2
+    o0, lse0 = k.attn_fwd(q, kk, v, H, D, mask)  # running-max kernel (no bound): another code path
+    assert (lse - lse0).abs().max().item() < 4e-3
+    assert rel(o, o0) < 5e-3
+    o2, lse2 = k.attn_fwd(q, kk, v, H, D, mask, score_bound=k.qk_norm_bound(D))
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+
+
 def test_attention_dit_v4_shape_smoke():
     """Full dit_v4 attention shape (24 heads x 98,304 tokens): finite, rows normalised."""
     k = K()
