@@ -89,6 +89,12 @@ int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const voi
  *   (i, D/2 + i); cos/sin fp32 tables [*, D/2] at row tab_off + (tpos_div ? t % tpos_div : t). */
 int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const float* cosb, const float* sinb,
                      long ld_tab, long tab_off, long tpos_div, void* out, long ldo, float* rstd, void* stream);
+/* decode form (attn.py:86-104 cache branch): q and k rotated as above, v copied, each into its own
+ * destination (row stride ld*, batch stride s*; token t -> batch t / L, row t % L): k and v go
+ * straight into the KV cache behind its window; no rstd */
+int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
+                        const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
+                        long ldko, long sko, void* vo, long ldvo, long svo, void* stream);
 int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
                      const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
                      const float* rstd, void* dqkv, long ldg, void* stream);

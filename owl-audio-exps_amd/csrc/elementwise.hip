@@ -263,6 +263,51 @@ __global__ __launch_bounds__(256) void qk_rope_fwd_k(const bf16* __restrict__ qk
   *(bf16x4*)(o + D / 2 + j * 4) = y1;
 }
 
+// decode form: the same q / k rotation with q, k and a copy of v written to three destinations with
+// their own row and batch strides (token t of batch t / L, row t % L) -- k and v straight into the
+// KV cache's slots behind the cached window, so the decode step needs no separate cache copies
+template <int D>
+__global__ __launch_bounds__(256) void qk_rope_kv_k(const bf16* __restrict__ qkv, long ldq, long T, long L, int H,
+                                                    const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                    long ld_tab, long tab_off, bf16* __restrict__ qo, long ldqo,
+                                                    long sqo, bf16* __restrict__ ko, long ldko, long sko,
+                                                    bf16* __restrict__ vo, long ldvo, long svo) {
+  constexpr int CPR = D / 8;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long rowid = gid / CPR;  // (token, which, head)
+  const int j = gid % CPR;
+  if (rowid >= T * 3 * H) return;
+  const long tok = rowid / (3 * H);
+  const int wh = rowid % (3 * H);  // which * H + head
+  const long bb = tok / L, t = tok - bb * L;
+  const bf16x8 v = *(const bf16x8*)(qkv + tok * ldq + (long)wh * D + j * 8);
+  if (wh >= 2 * H) {  // v: copied as is
+    *(bf16x8*)(vo + bb * svo + t * ldvo + (long)(wh - 2 * H) * D + j * 8) = v;
+    return;
+  }
+  float xv[8];
+  unpack8(v, xv);
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ss += xv[e] * xv[e];
+#pragma unroll
+  for (int o = 1; o < CPR; o <<= 1) ss += __shfl_xor(ss, o, 64);
+  const float r = rsqrtf(ss / D + RMS_EPS);
+  const long pos = tab_off + t;
+  const f32x4 c = *(const f32x4*)(cosb + pos * ld_tab + j * 4);
+  const f32x4 s = *(const f32x4*)(sinb + pos * ld_tab + j * 4);
+  bf16x4 y0, y1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = rb(xv[2 * i] * r), x1 = rb(xv[2 * i + 1] * r);
+    y0[i] = (bf16)(x0 * c[i] - x1 * s[i]);
+    y1[i] = (bf16)(x1 * c[i] + x0 * s[i]);
+  }
+  bf16* o = wh < H ? qo + bb * sqo + t * ldqo + (long)wh * D : ko + bb * sko + t * ldko + (long)(wh - H) * D;
+  *(bf16x4*)(o + j * 4) = y0;
+  *(bf16x4*)(o + D / 2 + j * 4) = y1;
+}
+
 // backward: d(q_rot) -> inverse rotation -> rms_norm backward (recomputing xhat from raw qkv)
 template <int D>
 __global__ __launch_bounds__(256) void qk_rope_bwd_k(const bf16* __restrict__ dqk, long ldd,
@@ -528,6 +573,25 @@ extern "C" int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D,
     hipLaunchKernelGGL(qk_rope_fwd_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, H, cosb,
                        sinb, ld_tab, tab_off, tpos_div, (bf16*)out, ldo, rstd);
   return owlk::check_launch("qk_rope_fwd");
+}
+
+extern "C" int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
+                                   const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo,
+                                   void* ko, long ldko, long sko, void* vo, long ldvo, long svo, void* stream) {
+  OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_fwd_kv: head_dim %d unsupported", D);
+  OWLK_REQUIRE(L > 0 && T % L == 0, "qk_rope_fwd_kv: T=%ld is not a whole number of L=%ld rows", T, L);
+  OWLK_REQUIRE(((uintptr_t)qo | (uintptr_t)ko | (uintptr_t)vo) % 16 == 0 && ldqo % 8 == 0 && ldko % 8 == 0 &&
+                   ldvo % 8 == 0 && sqo % 8 == 0 && sko % 8 == 0 && svo % 8 == 0,
+               "qk_rope_fwd_kv: destinations must be 16-byte aligned");
+  const long threads = T * 3 * H * (D / 8);
+  dim3 g((unsigned)((threads + 255) / 256));
+  if (D == 64)
+    hipLaunchKernelGGL(qk_rope_kv_k<64>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, L, H, cosb,
+                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo);
+  else
+    hipLaunchKernelGGL(qk_rope_kv_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, L, H, cosb,
+                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo);
+  return owlk::check_launch("qk_rope_fwd_kv");
 }
 
 extern "C" int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,

@@ -24,6 +24,7 @@ _SIGS = {
     "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
     "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],
     "owlk_qk_rope_fwd": [P, L, L, I, I, P, P, L, L, L, P, L, P, P],
+    "owlk_qk_rope_fwd_kv": [P, L, L, L, I, I, P, P, L, L, P, L, L, P, L, L, P, L, L, P],
     "owlk_qk_rope_bwd": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P],
     "owlk_attn_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, L, I, F, F, L, I, I, L, P, P, P, P, L, P],
     "owlk_attn_delta": [P, P, L, L, L, I, I, P, P],

@@ -163,6 +163,16 @@ def qk_rope_fwd(qkv, H, D, cos, sin, tab_off=0, tpos_div=0):
     return out, rstd
 
 
+def qk_rope_fwd_kv(qkv, B, L, H, D, cos, sin, tab_off, q_out, k_out, v_out):
+    """Decode form: qkv [B L, 3 H D] -> rotated q into q_out [B, L, H D], rotated k into k_out and
+    v copied into v_out (views of the KV cache's slots; any row / batch strides)."""
+    for t, nm in ((q_out, "q_out"), (k_out, "k_out"), (v_out, "v_out")):
+        assert t.shape == (B, L, H * D) and t.stride(2) == 1 and t.dtype == BF16, nm
+    call("owlk_qk_rope_fwd_kv", ptr(qkv), qkv.stride(0), B * L, L, H, D, ptr(cos), ptr(sin), cos.stride(0), tab_off,
+         ptr(q_out), q_out.stride(1), q_out.stride(0), ptr(k_out), k_out.stride(1), k_out.stride(0),
+         ptr(v_out), v_out.stride(1), v_out.stride(0), stream())
+
+
 def qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, dqkv, tab_off=0, tpos_div=0):
     T = qkv.shape[0]
     call("owlk_qk_rope_bwd", ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin),

@@ -94,10 +94,18 @@ class Attn(nn.Module):
         H = self.n_heads
         D = d // H
         offset = kv_cache.get_offset(self.layer_idx) if kv_cache is not None else 0
-        qkr, _ = K.qk_rope_fwd(qkv, H, D, self.rope.cos, self.rope.sin, offset, L)
-        q = qkr.view(B, L, 2 * d)[:, :, :d]
-        k = qkr.view(B, L, 2 * d)[:, :, d:]
-        v = qkv.view(B, L, 3 * d)[:, :, 2 * d:]
+        if offset > 0 and kv_cache.noise_caches == 0.0 and hasattr(kv_cache, "extend_slots"):
+            # decode: rotated k and v written straight into the cache's slots behind its window
+            q = torch.empty(B, L, d, device=qkv.device, dtype=torch.bfloat16)
+            ks, vs = kv_cache.extend_slots(self.layer_idx, L, q)
+            K.qk_rope_fwd_kv(qkv, B, L, H, D, self.rope.cos, self.rope.sin, offset, q, ks, vs)
+            k, v = kv_cache.extended(self.layer_idx, L)
+            offset = -1  # the [cache | new] views are in hand
+        else:
+            qkr, _ = K.qk_rope_fwd(qkv, H, D, self.rope.cos, self.rope.sin, offset, L)
+            q = qkr.view(B, L, 2 * d)[:, :, :d]
+            k = qkr.view(B, L, 2 * d)[:, :, d:]
+            v = qkv.view(B, L, 3 * d)[:, :, 2 * d:]
         if offset > 0:
             if kv_cache.noise_caches == 0.0 and hasattr(kv_cache, "extend"):
                 k, v = kv_cache.extend(self.layer_idx, k, v)  # [cache | new] in place, no torch.cat

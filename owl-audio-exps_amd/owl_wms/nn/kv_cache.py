@@ -82,6 +82,20 @@ class SingleKVCache:
             v = v + torch.randn_like(v) * self.noise_caches
         return k, v
 
+    def extend_slots(self, layer_ind, L, like):
+        """Views of the [B, L, d] slots behind the layer's cached window where the new frame's K/V go
+        (written there directly by the decode rope kernel); ``extended(layer_ind, L)`` then gives
+        [cache | new]."""
+        assert self.noise_caches == 0.0, "the slots are read as stored (noise_caches must be 0)"
+        n = self.len[layer_ind]
+        self._reserve(layer_ind, n + L, like)
+        kb, vb = self.bufs[layer_ind]
+        s = self.start[layer_ind]
+        return kb[:, s + n:s + n + L], vb[:, s + n:s + n + L]
+
+    def extended(self, layer_ind, L):
+        return self._views(layer_ind, self.len[layer_ind] + L)
+
     def extend(self, layer_ind, new_k, new_v):
         """[cache | new] as views of the layer's buffer (new K/V written once behind the cache)."""
         assert self.noise_caches == 0.0, "extend reads the cache as stored (noise_caches must be 0)"
