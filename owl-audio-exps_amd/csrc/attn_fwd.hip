@@ -487,7 +487,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_k(FwdP p) {
 // query's scores sit in column c, rows 4 g + r (g = lane >> 4); P feeds O^T += V^T P as the B
 // operand in the permuted key order (pack_perm), V^T read by frag_tr16.  Row sums stay per lane
 // group until the epilogue (4 partial sums per query, added across the groups there).
-template <bool UNUSED = true>
+template <bool RS>
 __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   using C = Cfg<64>;
   __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::TILEB + 16];
@@ -576,6 +576,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
 #pragma unroll
     for (int t4 = 0; t4 < 4; ++t4) o[ds][t4] = f32x4{0.f, 0.f, 0.f, 0.f};
   float lrow[4] = {0.f, 0.f, 0.f, 0.f};
+  // RS: row sums as one more MFMA per query tile and key half (ones^T P: every accumulator row
+  // holds the query's partial sum) instead of 16 VALU adds per query tile and key half
+  f32x4 lacc[4];
+#pragma unroll
+  for (int t4 = 0; t4 < 4; ++t4) lacc[t4] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
 
   const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_TR>(p.ldv, w, lane);
   auto issue = [&](char* buf, long c0) {
@@ -652,19 +660,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
         bf16x8 pf[4];
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4) {
-          float ps0 = 0.f, ps1 = 0.f;
+          if (RS) {
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
+            for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float pv = __builtin_amdgcn_exp2f(st[kk][t4][r]);
-              st[kk][t4][r] = pv;
-              if (r & 1)
-                ps1 += pv;
-              else
-                ps0 += pv;
-            }
-          lrow[t4] += ps0 + ps1;
+              for (int r = 0; r < 4; ++r) st[kk][t4][r] = __builtin_amdgcn_exp2f(st[kk][t4][r]);
+          } else {
+            float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float pv = __builtin_amdgcn_exp2f(st[kk][t4][r]);
+                st[kk][t4][r] = pv;
+                if (r & 1)
+                  ps1 += pv;
+                else
+                  ps0 += pv;
+              }
+            lrow[t4] += ps0 + ps1;
+          }
           pf[t4] = pack_perm(st[0][t4], st[1][t4]);
         }
 #pragma unroll
@@ -673,6 +688,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
 #pragma unroll
           for (int t4 = 0; t4 < 4; ++t4)
             o[ds][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pf[t4], o[ds][t4], 0, 0, 0);
+        }
+        if (RS) {
+#pragma unroll
+          for (int t4 = 0; t4 < 4; ++t4)
+            lacc[t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[t4], lacc[t4], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);  // one key half's S / P live at a time (register budget)
       }
@@ -683,8 +703,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
 
 #pragma unroll
   for (int t4 = 0; t4 < 4; ++t4) {
-    float ltot = lrow[t4] + __shfl_xor(lrow[t4], 16, 64);
-    ltot += __shfl_xor(ltot, 32, 64);
+    float ltot;
+    if (RS) {
+      ltot = lacc[t4][0];  // every row of ones^T P holds the full sum over the keys
+    } else {
+      ltot = lrow[t4] + __shfl_xor(lrow[t4], 16, 64);
+      ltot += __shfl_xor(ltot, 32, 64);
+    }
     if (my_q[t4] < p.Lq) {
       const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
       bf16* O = p.o + b * p.sob + my_q[t4] * p.ldo + head * 64 + 4 * g;
@@ -868,6 +893,7 @@ template <int D>
 void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   static const int two = getenv("OWLK_FWD2") ? atoi(getenv("OWLK_FWD2")) : 1;
   static const int f16 = getenv("OWLK_FWD16") ? atoi(getenv("OWLK_FWD16")) : 1;  // 16x16x32 variant (0: off)
+  static const int rs = getenv("OWLK_FWD_RS") ? atoi(getenv("OWLK_FWD_RS")) : 1;  // row sums on the MFMA (0: VALU adds)
   // decode: one unmasked <= 64-query block per (batch, head) over >= 4 key tiles
   static const int split = getenv("OWLK_FWD_SPLIT") ? atoi(getenv("OWLK_FWD_SPLIT")) : 1;
   const MaskP& m = p.m;
@@ -878,7 +904,10 @@ void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   }
   if (D == 64 && f16 && p.bound > 0.f) {
     const dim3 g2((unsigned)((p.Lq + QT2 - 1) / QT2), grid.y, grid.z);
-    hipLaunchKernelGGL((attn_fwd16_k<true>), g2, dim3(256), 0, s, p);
+    if (rs)
+      hipLaunchKernelGGL((attn_fwd16_k<true>), g2, dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_fwd16_k<false>), g2, dim3(256), 0, s, p);
     return;
   }
   if (D == 64 && two) {
