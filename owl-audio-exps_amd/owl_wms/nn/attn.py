@@ -16,7 +16,7 @@ from torch import nn
 from torch.utils.checkpoint import checkpoint as torch_checkpoint
 
 from .. import kernels as K
-from .fused import BlockGeometry, DiTBlockFn, adaln, bf16_weight, linear
+from .fused import BlockGeometry, DiTBlockFn, ModFn, adaln, bf16_weight, linear, stacked_modulation_weights
 from .mlp import MLP
 from .modulation import AdaLN, Gate
 from .rope import get_rope_cls
@@ -138,8 +138,12 @@ class DiTBlock(nn.Module):
         self.config = config
 
     def modulation(self, cond):
-        s = F.silu(cond)
-        return self.adaln1.mod(s), self.gate1.mod(s), self.adaln2.mod(s), self.gate2.mod(s)
+        """(adaln1 [2d], gate1 [d], adaln2 [2d], gate2 [d]) per frame from silu(cond): one stacked GEMM
+        (fused.ModFn) instead of the four Linears."""
+        ws, bs = self.mod_params()
+        params = [t for pair in zip(ws, bs) for t in pair]
+        W, bvec = stacked_modulation_weights(self, params)
+        return ModFn.apply(F.silu(cond), W, bvec, *params)
 
     def mod_params(self):
         """(weights, biases) of the four per-frame modulation Linears, in the column order of

@@ -292,6 +292,62 @@ class DiTBlockFn(torch.autograd.Function):
                 dwqkv, dbqkv, dwout, dbout, dw1, db1, dw2, db2, None)
 
 
+class ModFn(torch.autograd.Function):
+    """DiTBlock.modulation: the fc's of adaln1, gate1, adaln2 and gate2 (modulation.py:13-40) all read
+    the same silu(cond), so they run as ONE GEMM against the four weights stacked [6d, d] (bf16,
+    with the biases stacked fp32).  The outputs are column views [2d | d | 2d | d] of that one
+    result.  Backward: the four output gradients (bf16-rounded, as the Linears' own backward would)
+    go into one [F, 6d] matrix; ONE dX GEMM against the stack replaces four GEMMs and autograd's
+    three adds; the weight / bias gradients go into each parameter's bucket view as before."""
+
+    @staticmethod
+    def forward(ctx, s, wstack, bstack, *params):
+        b, n, d = s.shape
+        x2 = s.reshape(-1, d).to(BF16).contiguous()
+        y = K.gemm(x2, wstack, bias=bstack).view(b, n, 6 * d)
+        ctx.save_for_backward(x2, wstack)
+        ctx.params, ctx.shp = params, (b, n, d)
+        return y[..., :2 * d], y[..., 2 * d:3 * d], y[..., 3 * d:5 * d], y[..., 5 * d:]
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        x2, wstack = ctx.saved_tensors
+        b, n, d = ctx.shp
+        F_ = b * n
+        cols = ((0, 2 * d), (2 * d, 3 * d), (3 * d, 5 * d), (5 * d, 6 * d))
+        dm = torch.empty(F_, 6 * d, device=x2.device, dtype=BF16)
+        for g, (lo, hi) in zip(gouts, cols):
+            if g is None:
+                dm[:, lo:hi].zero_()
+            else:
+                dm[:, lo:hi].copy_(g.reshape(F_, hi - lo))
+        ds = None
+        if ctx.needs_input_grad[0]:
+            # K = 6d is long against a [F, d] output (36 256^2 tiles): the fp32 form takes the split-K
+            # plan (partials + ordered reduce), ~4x faster than one pass of small tiles
+            ds = K.gemm(dm, wstack, b_trans=True, out_f32=True).to(BF16).view(b, n, d)
+        grads = []
+        for i, (lo, hi) in enumerate(cols):
+            w, bias = ctx.params[2 * i], ctx.params[2 * i + 1]
+            dmi = dm[:, lo:hi]
+            grads.append(wgrad_into(w, dmi, x2) if w.requires_grad else None)
+            grads.append(bgrad_into(bias, dmi) if bias is not None and bias.requires_grad else None)
+        return (ds, None, None, *grads)
+
+
+def stacked_modulation_weights(owner, params):
+    """bf16 [6d, d] stack of the four modulation weights and fp32 [6d] stack of their biases, cached
+    on `owner` and rebuilt when a parameter's version (an optimizer step) or identity changes."""
+    key = tuple((id(p), p._version, p.device) for p in params)
+    ent = getattr(owner, "_owl_mod_stack", None)
+    if ent is None or ent[0] != key:
+        W = torch.cat([params[2 * i].detach().to(BF16) for i in range(4)]).contiguous()
+        bvec = torch.cat([params[2 * i + 1].detach().float() for i in range(4)]).contiguous()
+        ent = (key, W, bvec)
+        object.__setattr__(owner, "_owl_mod_stack", ent)
+    return ent[1], ent[2]
+
+
 class LayerNormFn(torch.autograd.Function):
     """F.layer_norm(x, (d,)).type_as(x) (normalization.py:6-7): fp32 math, bf16 out, libowlk."""
 
