@@ -744,6 +744,17 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
   if (wr == 0) OWLK_PP_BAR();  // pairs with group 1's final barrier: every MFMA / LDS read done
 #undef OWLK_PP_BAR
 #undef OWLK_PP_SYNC
+#ifdef OWLK_GEMM_EXP_NOEPI  // timing experiment only (tools/build_variant.sh -DOWLK_GEMM_EXP_NOEPI)
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0];
+    if (t == 1234.5f) ((float*)p.C)[threadIdx.x] = t;
+    return;
+  }
+#endif
 
   // ---- epilogue per wave through a private 16 x 64 fp32 LDS strip (reuses the staging ring).
   // Each lane owns one 8-column chunk (fixed for the whole tile): its bias is loaded once, and the

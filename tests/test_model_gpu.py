@@ -610,3 +610,41 @@ def test_optimizer_step_refreshes_bf16_weights():
             outs.append(mm(GR[p + "in.x"].cuda(), GR[p + "in.mouse"].cuda(), GR[p + "in.btn"].cuda(),
                            GR[p + "in.doc_id"].cuda(), return_dict=True)["pred_video"])
     assert torch.equal(outs[0], outs[1])
+
+
+def test_stacked_modulation_matches_four_linears():
+    """fused.ModFn (DiTBlock.modulation: the four per-frame Linears of adaln1, gate1, adaln2, gate2 as
+    one stacked GEMM with one dX GEMM in backward) == the four Linears on libowlk (nn/fused.linear):
+    outputs, the cond gradient and every weight / bias gradient within bf16 GEMM tolerance."""
+    import torch.nn.functional as F
+    from owl_wms.nn.fused import ModFn, linear, stacked_modulation_weights
+    torch.manual_seed(3)
+    d, b, n = 256, 2, 24
+    shapes = (2 * d, d, 2 * d, d)
+    base = []
+    for o in shapes:
+        base += [torch.randn(o, d) * d ** -0.5, torch.randn(o) * 0.1]
+    rs = [torch.randn(b, n, o, device="cuda") for o in shapes]
+    cond0 = torch.randn(b, n, d)
+
+    def run(stacked):
+        ps = [torch.nn.Parameter(t.clone().cuda()) for t in base]
+        cond = cond0.clone().cuda().requires_grad_(True)
+        s = F.silu(cond)
+        if stacked:
+            owner = torch.nn.Module()
+            W, bv = stacked_modulation_weights(owner, ps)
+            outs = ModFn.apply(s, W, bv, *ps)
+        else:
+            outs = [linear(s, ps[2 * i], ps[2 * i + 1]) for i in range(4)]
+        loss = sum((o.float() * r).sum() for o, r in zip(outs, rs))
+        loss.backward()
+        return [o.detach().float() for o in outs], cond.grad.float(), [p.grad.float() for p in ps]
+
+    o1, c1, g1 = run(True)
+    o2, c2, g2 = run(False)
+    for a, r in zip(o1, o2):
+        assert rel(a, r) < 1e-2
+    assert rel(c1, c2) < 1e-2
+    for a, r in zip(g1, g2):
+        assert rel(a, r) < 1e-2
