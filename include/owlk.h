@@ -95,6 +95,12 @@ int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const floa
 int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
                         const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
                         long ldko, long sko, void* vo, long ldvo, long svo, void* stream);
+/* the same with the cache position on the device: state = {start, cached tokens, rope offset}
+ * (int64), k / v written to rows start + cached + t of kbuf / vbuf, rope position offset + t; one
+ * captured HIP graph then serves every frame of a growing cache */
+int owlk_qk_rope_fwd_kv_dev(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
+                            const float* sinb, long ld_tab, const long* state, void* qo, long ldqo, long sqo,
+                            void* kbuf, long ldk, long skb, void* vbuf, long ldv, long svb, void* stream);
 int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
                      const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
                      const float* rstd, void* dqkv, long ldg, void* stream);
@@ -116,6 +122,15 @@ int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, lo
                   long q_offset,
                   const int* kv_lo, const int* q_hi, const int* run_start, const int* doc, long fstride,
                   void* stream);
+/* Decode attention (attn.py:86-107 cache branch) with the cache position on the device: one frame
+ * of Lq <= 64 queries per (batch, head), unmasked over [cache | Lnew new rows] of the cache
+ * buffers kbuf / vbuf (the new rows written there first, owlk_qk_rope_fwd_kv_dev), or over the
+ * last window_tokens of them (windowed layer; 0: all); state = {start, cached tokens, rope offset}
+ * int64 on the device.  head_dim 64, bounded softmax (score_bound > 0) only. */
+int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const void* kbuf, long ldk, long skb,
+                         const void* vbuf, long ldv, long svb, void* o, long ldo, long sob, float* lse, long B,
+                         int H, long Lq, int head_dim, float scale, float score_bound, const long* state,
+                         long Lnew, long window_tokens, void* stream);
 /* delta[b, h, t] = sum_d dO * O (fp32), the backward's row constant */
 int owlk_attn_delta(const void* o, const void* dout, long ld, long B, long L, int H, int D, float* delta,
                     void* stream);

@@ -731,7 +731,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
 // the key tiles (wave w takes tiles w, w + 4, ...), each streaming its tiles by LDS-DMA into a
 // private 2-slot ring (no barriers in the sweep); with the bounded softmax (no running maximum)
 // the waves' partial O and row sums simply add, in wave order, through LDS at the end.
-__global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p) {
+__global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long* __restrict__ state, long Lnew,
+                                                             long wtok) {
+  // device-resident cache state (owlk_attn_decode_fwd): {start, cached tokens, rope offset} of the
+  // cache buffers p.k / p.v, so one captured HIP graph serves every frame of a growing cache; the
+  // keys are [cache | the Lnew new rows], the last wtok of them for a windowed layer (wtok > 0)
+  if (state) {
+    const long start = state[0], total = state[1] + Lnew;
+    const long first = wtok > 0 && total > wtok ? total - wtok : 0;
+    p.k += (start + first) * p.ldk;
+    p.v += (start + first) * p.ldv;
+    p.Lkv = total - first;
+  }
   using C = Cfg<64>;
   constexpr int RING = 2 * C::TILEB;  // per wave
   constexpr int OLD = 68;             // fp32 row stride of the combine image
@@ -899,7 +910,8 @@ void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   const MaskP& m = p.m;
   if (D == 64 && split && p.bound > 0.f && p.Lq <= 64 && p.Lkv >= 4 * KT && m.window == 0 && !m.causal &&
       !m.kv_lo && !m.doc && m.q_offset == 0) {
-    hipLaunchKernelGGL(attn_fwd16_split_k, dim3(1, grid.y, grid.z), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(attn_fwd16_split_k, dim3(1, grid.y, grid.z), dim3(256), 0, s, p, (const long*)nullptr, 0L,
+                       0L);
     return;
   }
   if (D == 64 && f16 && p.bound > 0.f) {
@@ -970,4 +982,27 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
   else
     launch_fwd<128>(p, grid, (hipStream_t)stream);
   return owlk::check_launch("attn_fwd");
+}
+
+extern "C" int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const void* kbuf, long ldk, long skb,
+                                    const void* vbuf, long ldv, long svb, void* o, long ldo, long sob, float* lse,
+                                    long B, int H, long Lq, int head_dim, float scale, float score_bound,
+                                    const long* state, long Lnew, long window_tokens, void* stream) {
+  OWLK_REQUIRE(head_dim == 64, "attn_decode_fwd: head_dim %d not built (64)", head_dim);
+  OWLK_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lq <= 64 && Lnew > 0 && state, "attn_decode_fwd: bad sizes");
+  OWLK_REQUIRE(score_bound > 0.f && score_bound * scale < 40.f, "attn_decode_fwd: needs a score bound");
+  OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)kbuf | (uintptr_t)vbuf | (uintptr_t)o) % 16 == 0 && ldq % 8 == 0 &&
+                   ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0,
+               "attn_decode_fwd: q/k/v/o rows must be 16-byte aligned");
+  FwdP p;
+  p.q = (const bf16*)q; p.k = (const bf16*)kbuf; p.v = (const bf16*)vbuf; p.o = (bf16*)o; p.lse = lse;
+  p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
+  p.sqb = sqb; p.skb = skb; p.svb = svb; p.sob = sob;
+  p.Lq = Lq; p.Lkv = 0; p.H = H;  // Lkv from the device state
+  p.scale_log2 = scale * LOG2E;
+  p.bound = score_bound;
+  p.m = owlk_make_mask(1, 0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, 0);
+  hipLaunchKernelGGL(attn_fwd16_split_k, dim3(1, (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream, p,
+                     state, Lnew, window_tokens);
+  return owlk::check_launch("attn_decode_fwd");
 }

@@ -271,7 +271,14 @@ __global__ __launch_bounds__(256) void qk_rope_kv_k(const bf16* __restrict__ qkv
                                                     const float* __restrict__ cosb, const float* __restrict__ sinb,
                                                     long ld_tab, long tab_off, bf16* __restrict__ qo, long ldqo,
                                                     long sqo, bf16* __restrict__ ko, long ldko, long sko,
-                                                    bf16* __restrict__ vo, long ldvo, long svo) {
+                                                    bf16* __restrict__ vo, long ldvo, long svo,
+                                                    const long* __restrict__ state) {
+  if (state) {  // {start, cached tokens, rope offset}: k / v rows go behind the window of the buffers
+    const long row0 = state[0] + state[1];
+    ko += row0 * ldko;
+    vo += row0 * ldvo;
+    tab_off = state[2];
+  }
   constexpr int CPR = D / 8;
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const long rowid = gid / CPR;  // (token, which, head)
@@ -575,9 +582,29 @@ extern "C" int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D,
   return owlk::check_launch("qk_rope_fwd");
 }
 
+static int qk_rope_kv_launch(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
+                             const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
+                             long ldko, long sko, void* vo, long ldvo, long svo, const long* state, void* stream);
+
 extern "C" int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
                                    const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo,
                                    void* ko, long ldko, long sko, void* vo, long ldvo, long svo, void* stream) {
+  return qk_rope_kv_launch(qkv, ldq, T, L, H, D, cosb, sinb, ld_tab, tab_off, qo, ldqo, sqo, ko, ldko, sko, vo, ldvo,
+                           svo, nullptr, stream);
+}
+
+extern "C" int owlk_qk_rope_fwd_kv_dev(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
+                                       const float* sinb, long ld_tab, const long* state, void* qo, long ldqo,
+                                       long sqo, void* kbuf, long ldk, long skb, void* vbuf, long ldv, long svb,
+                                       void* stream) {
+  OWLK_REQUIRE(state, "qk_rope_fwd_kv_dev: state pointer required");
+  return qk_rope_kv_launch(qkv, ldq, T, L, H, D, cosb, sinb, ld_tab, 0, qo, ldqo, sqo, kbuf, ldk, skb, vbuf, ldv, svb,
+                           state, stream);
+}
+
+static int qk_rope_kv_launch(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
+                             const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
+                             long ldko, long sko, void* vo, long ldvo, long svo, const long* state, void* stream) {
   OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_fwd_kv: head_dim %d unsupported", D);
   OWLK_REQUIRE(L > 0 && T % L == 0, "qk_rope_fwd_kv: T=%ld is not a whole number of L=%ld rows", T, L);
   OWLK_REQUIRE(((uintptr_t)qo | (uintptr_t)ko | (uintptr_t)vo) % 16 == 0 && ldqo % 8 == 0 && ldko % 8 == 0 &&
@@ -587,10 +614,10 @@ extern "C" int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, in
   dim3 g((unsigned)((threads + 255) / 256));
   if (D == 64)
     hipLaunchKernelGGL(qk_rope_kv_k<64>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, L, H, cosb,
-                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo);
+                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo, state);
   else
     hipLaunchKernelGGL(qk_rope_kv_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, L, H, cosb,
-                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo);
+                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo, state);
   return owlk::check_launch("qk_rope_fwd_kv");
 }
 

@@ -173,6 +173,32 @@ def qk_rope_fwd_kv(qkv, B, L, H, D, cos, sin, tab_off, q_out, k_out, v_out):
          ptr(v_out), v_out.stride(1), v_out.stride(0), stream())
 
 
+def qk_rope_fwd_kv_dev(qkv, B, L, H, D, cos, sin, state, q_out, kbuf, vbuf):
+    """qk_rope_fwd_kv with the cache position on the device (state int64 {start, cached, offset}):
+    k / v go to rows start + cached + t of the cache buffers kbuf / vbuf [B, cap, H D]."""
+    assert state.dtype == torch.int64 and state.numel() >= 3 and state.is_cuda
+    assert q_out.shape == (B, L, H * D) and q_out.stride(2) == 1
+    for t in (kbuf, vbuf):
+        assert t.dim() == 3 and t.shape[0] == B and t.shape[2] == H * D and t.stride(2) == 1 and t.dtype == BF16
+    call("owlk_qk_rope_fwd_kv_dev", ptr(qkv), qkv.stride(0), B * L, L, H, D, ptr(cos), ptr(sin), cos.stride(0),
+         ptr(state), ptr(q_out), q_out.stride(1), q_out.stride(0), ptr(kbuf), kbuf.stride(1), kbuf.stride(0),
+         ptr(vbuf), vbuf.stride(1), vbuf.stride(0), stream())
+
+
+def attn_decode_fwd(q, kbuf, vbuf, H, D, state, Lnew, window_tokens=0, scale=None, score_bound=0.0):
+    """Decode attention over the cache buffers with the cache position on the device (state, see
+    qk_rope_fwd_kv_dev): q [B, Lq <= 64, H D] against [cache | Lnew new rows] (or its last
+    window_tokens rows) -> o [B, Lq, H D], lse [B, H, Lq] (base 2)."""
+    B, Lq, _ = q.shape
+    o = torch.empty_like(q)
+    lse = torch.empty(B, H, Lq, device=q.device, dtype=F32)
+    call("owlk_attn_decode_fwd", ptr(q), q.stride(1), q.stride(0), ptr(kbuf), kbuf.stride(1), kbuf.stride(0),
+         ptr(vbuf), vbuf.stride(1), vbuf.stride(0), ptr(o), o.stride(1), o.stride(0), ptr(lse), B, H, Lq, D,
+         float(scale if scale is not None else D ** -0.5), float(score_bound), ptr(state), Lnew, window_tokens,
+         stream())
+    return o, lse
+
+
 def qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, dqkv, tab_off=0, tpos_div=0):
     T = qkv.shape[0]
     call("owlk_qk_rope_bwd", ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin),

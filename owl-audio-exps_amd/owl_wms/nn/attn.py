@@ -94,6 +94,16 @@ class Attn(nn.Module):
         H = self.n_heads
         D = d // H
         offset = kv_cache.get_offset(self.layer_idx) if kv_cache is not None else 0
+        if block_mask is None and getattr(kv_cache, "dev", None) is not None and offset > 0:
+            # decode with the cache position on the device (one captured graph for every frame)
+            kb, vb = kv_cache.bufs[self.layer_idx]
+            q = torch.empty(B, L, d, device=qkv.device, dtype=torch.bfloat16)
+            K.qk_rope_fwd_kv_dev(qkv, B, L, H, D, self.rope.cos, self.rope.sin, kv_cache.dev, q, kb, vb)
+            o, _ = K.attn_decode_fwd(q, kb, vb, H, D, kv_cache.dev, L, self.local_offset if self.local else 0,
+                                     score_bound=K.qk_norm_bound(D))
+            if kv_cache.should_update:
+                kv_cache.commit_device(self.layer_idx, L)
+            return o
         if offset > 0 and kv_cache.noise_caches == 0.0 and hasattr(kv_cache, "extend_slots"):
             # decode: rotated k and v written straight into the cache's slots behind its window
             q = torch.empty(B, L, d, device=qkv.device, dtype=torch.bfloat16)
@@ -233,6 +243,8 @@ class DiT(nn.Module):
             ck = ckpt and (n_ck is None or i < n_ck)
             block._checkpointed = ck  # the re-run inside backward reuses the kept attention output
             x = checkpoint(block, x, cond, mask, kv_cache) if ck else block(x, cond, mask, kv_cache)
+        if kv_cache is not None and kv_cache.should_update and getattr(kv_cache, "dev", None) is not None:
+            kv_cache.sync_device_state()  # every layer committed the frame
         return x
 
     @torch.no_grad()

@@ -29,6 +29,45 @@ class SingleKVCache:
         self.offsets = [0] * config.n_layers
         self.start = [0] * config.n_layers
         self.len = [0] * config.n_layers
+        self.dev = None  # device state {start, cached tokens, rope offset} (enable_device_state)
+
+    def enable_device_state(self, capacity):
+        """Decode with the cache position on the device: every layer's buffer is reserved for
+        `capacity` tokens (no reallocation or compaction while sampling: fixed addresses), and the
+        decode kernels read {start, cached tokens, rope offset} from an int64 device vector, so a
+        HIP graph captured once serves every frame while the cache grows.  All layers advance
+        together in decode, so one vector describes them all."""
+        for i in range(self.config.n_layers):
+            kb = self.bufs[i]
+            assert kb is not None, "enable_device_state after the context pass"
+            if kb[0].shape[1] < capacity:
+                n, s = self.len[i], self.start[i]
+                new = tuple(torch.empty(kb[0].shape[0], capacity, kb[0].shape[2], device=kb[0].device,
+                                        dtype=kb[0].dtype) for _ in range(2))
+                if n:
+                    for dst, src in zip(new, (kb[0][:, s:s + n], kb[1][:, s:s + n])):
+                        dst[:, :n].copy_(src)
+                self.bufs[i], self.start[i] = new, 0
+        self.dev = torch.zeros(4, dtype=torch.int64, device=self.bufs[0][0].device)
+        self.sync_device_state()
+
+    def sync_device_state(self):
+        """host position -> the device vector (outside graph capture: an H2D copy)"""
+        if self.dev is None:
+            return
+        st = {(self.start[i], self.len[i], self.offsets[i]) for i in range(self.config.n_layers)}
+        assert len(st) == 1, "device-state decode needs every layer at the same position"
+        s, n, o = st.pop()
+        assert s + n <= self.bufs[0][0].shape[1]
+        self.dev.copy_(torch.tensor([s, n, o, 0], dtype=torch.int64))
+
+    def commit_device(self, layer_ind, L):
+        """host bookkeeping of a device-state decode step that wrote L new rows behind the window
+        (the device vector is refreshed once per forward, sync_device_state)"""
+        assert self.start[layer_ind] + self.len[layer_ind] + L <= self.bufs[layer_ind][0].shape[1], \
+            "cache capacity exceeded (enable_device_state(capacity))"
+        self.len[layer_ind] += L
+        self.offsets[layer_ind] += L
 
     def enable_cache_updates(self):
         self.should_update = True
@@ -42,6 +81,7 @@ class SingleKVCache:
 
     def reset(self, batch_size=1):
         self.batch_size = batch_size
+        self.dev = None
         self.bufs = [None] * self.config.n_layers
         self.offsets = [0] * self.config.n_layers
         self.start = [0] * self.config.n_layers
@@ -134,6 +174,7 @@ class SingleKVCache:
             if not front:
                 self.start[i] += amt_i
             self.len[i] -= amt_i
+        self.sync_device_state()
 
     def length_at(self, idx):
         return self.len[idx]

@@ -29,6 +29,10 @@ class AVCachingSamplerV2:
         self.max_window = max_window
         self.custom_schedule = custom_schedule
         self._pool = None  # graph memory pool shared by the per-frame captures (compile_on_decode)
+        self._step_graph = None
+        # keep the cache position on the device so one captured Euler step serves every frame
+        # (False: the host-position path, one capture per frame with the cache length baked in)
+        self.device_state = True
 
     @staticmethod
     def zlerp(x, alpha):
@@ -80,6 +84,45 @@ class AVCachingSamplerV2:
         del g
         return sx.clone(), st.clone()
 
+    def _euler_replay(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
+        """compile_on_decode with the cache position on the device (SingleKVCache.enable_device_state):
+        ONE Euler step is captured on the first frame and replayed for every step of every frame
+        (its inputs are copied into the graph's static buffers first; the decode kernels read the
+        growing cache's position from the device).  The cache-update forward between frames stays
+        eager: its launches overlap the replays still running on the GPU."""
+        st = self._step_graph
+        first = 0
+        if st is None:
+            # first frame: step 0 eagerly (bf16 weight copies, workspaces outside the graph pool)
+            x, t = self._euler_step(model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt[0])
+            if self.n_steps == 1:
+                return x, t
+            bufs = {"x": x.clone(), "t": t.clone(), "dt": dt[1].clone(), "mouse": mouse.clone(), "btn": btn.clone(),
+                    "nm": null_mouse.clone(), "nb": null_btn.clone()}
+            if self._pool is None:
+                self._pool = torch.cuda.graph_pool_handle()
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, pool=self._pool, stream=side):
+                    nx, nt = self._euler_step(model, kv_cache, bufs["x"], bufs["t"], bufs["mouse"], bufs["btn"],
+                                              bufs["nm"], bufs["nb"], bufs["dt"])
+                    bufs["x"].copy_(nx)
+                    bufs["t"].copy_(nt)
+            torch.cuda.current_stream().wait_stream(side)
+            self._step_graph = st = (g, bufs)
+            first = 1
+        else:
+            g, bufs = st
+            for k, v in (("x", x), ("t", t), ("mouse", mouse), ("btn", btn)):
+                bufs[k].copy_(v)
+        g, bufs = st
+        for t_idx in range(first, self.n_steps):
+            bufs["dt"].copy_(dt[t_idx])
+            g.replay()
+        return bufs["x"].clone(), bufs["t"].clone()
+
     @torch.no_grad()
     def __call__(self, model, x, mouse, btn, compile_on_decode=False):
         """model: a GameRFTCore ([b,n,c,h,w] latents, kv_cache API); returns [b, init+new, c, h, w]."""
@@ -105,6 +148,12 @@ class AVCachingSamplerV2:
         kv_cache.disable_cache_updates()
 
         num_frames = min(self.num_frames, mouse.size(1) - init_len)
+        self._step_graph = None
+        # the cache position on the device (one captured step for every frame); the same kernels run
+        # in eager mode too, so eager and graphed decode stay bit-identical
+        dev_state = self.device_state and hasattr(kv_cache, "enable_device_state")
+        if dev_state:  # room for every frame up front: fixed buffer addresses for the one graph
+            kv_cache.enable_device_state((init_len + num_frames + 1) * model.config.tokens_per_frame)
         model.transformer.enable_decoding()
         try:
             for idx in range(num_frames):
@@ -112,7 +161,10 @@ class AVCachingSamplerV2:
                 start = init_len + idx
                 curr_mouse, curr_btn = mouse[:, start:start + 1], btn[:, start:start + 1]
                 null_mouse, null_btn = torch.zeros_like(curr_mouse), torch.zeros_like(curr_btn)
-                if compile_on_decode:
+                if dev_state and compile_on_decode:
+                    curr_x, curr_t = self._euler_replay(model, kv_cache, curr_x, curr_t, curr_mouse, curr_btn,
+                                                        null_mouse, null_btn, dt)
+                elif compile_on_decode:
                     curr_x, curr_t = self._euler_graphed(model, kv_cache, curr_x, curr_t, curr_mouse, curr_btn,
                                                          null_mouse, null_btn, dt, warm=idx == 0)
                 else:
@@ -129,4 +181,5 @@ class AVCachingSamplerV2:
                     kv_cache.truncate(1, front=False)
         finally:
             model.transformer.disable_decoding()
+            self._step_graph = None
         return torch.cat(latents, dim=1)

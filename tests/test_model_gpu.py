@@ -446,6 +446,27 @@ def test_graphed_decode_equals_eager(n_steps, cfg, custom):
     assert torch.equal(outs[0], outs[1])
 
 
+def test_device_state_decode_matches_host_state():
+    """AVCachingSamplerV2 with the cache position on the device (owlk_qk_rope_fwd_kv_dev +
+    owlk_attn_decode_fwd: one captured step for every frame) == the host-position decode path
+    (lengths baked into each launch), eager, within attention summation order; the graphed
+    device-state run equals its eager run bit for bit (test_graphed_decode_equals_eager)."""
+    from owl_wms.sampling import get_sampler_cls
+    m = _model().eval()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 4, 32, 8, 8, generator=g).bfloat16().cuda()
+    mouse = torch.randn(2, 9, 2, generator=g).bfloat16().cuda()
+    btn = (torch.rand(2, 9, 11, generator=g) < 0.5).bfloat16().cuda()
+    outs = []
+    for dev in (False, True):
+        torch.manual_seed(321)
+        s = get_sampler_cls("av_caching")(n_steps=4, cfg_scale=1.3, num_frames=5, noise_prev=0.2)
+        s.device_state = dev
+        outs.append(s(m.core, x, mouse, btn).float())
+    assert rel(outs[1], outs[0]) < 2e-2
+    assert torch.isfinite(outs[1]).all()
+
+
 def _dp_worker(rank, ws, port, q):
     import os as _os
     _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
