@@ -207,9 +207,15 @@ def main():
     traffic = {}
     if rank == 0 and world == 1 and not args.no_traffic and not args.no_profile:
         traffic = pmc_traffic(args)  # before this process initialises the GPU
+    if os.environ.get("OWL_BENCH_SHARE_GPU") == "1":
+        # rehearsal of the multi-rank path on a box with fewer GPUs than ranks (tools/rccl_rehearsal.sh)
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("OWL_BENCH_SHARE_GPU") == "1":  # RCCL refuses two ranks on one device
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
 
     from owl_wms import _lib
