@@ -210,6 +210,8 @@ ATTN_CASES = [
     (1, 2, 7, 65, None, False),  # unwindowed, ragged inside the second 64-row half of a 128-row dK/dV tile
     (2, 2, 8, 64, None, "split"),  # documents that recur (not one contiguous run): general doc path
     (1, 2, 12, 64, 4, "split"),
+    (1, 2, 24, 64, None, False),  # unwindowed sweeps of 12 query tiles (dK/dV ping-pong ring wraps)
+    (1, 1, 300, 1, None, False),  # token-causal: PARTIAL tiles on every diagonal, ragged end
 ]
 
 
