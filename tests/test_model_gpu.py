@@ -5,12 +5,12 @@ Tolerances (bf16 autocast semantics on both sides):
   measured <= 5e-3) and grad norms within 5e-2 (both modes),
   config-1 10-step loss trajectory within 2e-2 relative per step (GPU bf16 vs reference fp32).
 """
+import math
+import os
 from types import SimpleNamespace
 
 import pytest
 import torch
-
-import os
 
 from conftest import REPO, golden
 from oracle.params import det_init_, det_tensor
@@ -589,6 +589,63 @@ def test_trainer_resume_equals_uninterrupted(tmp_path):
         for i, st in sa[part]["state"].items():
             for kk, v in st.items():
                 assert torch.equal(v, sb[part]["state"][i][kk]), (part, i, kk)
+
+
+def _trainer_worker(rank, ws, port, q, cfg_path):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=ws)  # one card, 2 ranks: gloo on GPU tensors
+    try:
+        from owl_wms.configs import Config
+        from owl_wms.trainers import get_trainer_cls
+        torch.cuda.set_device(0)
+        c = Config.from_yaml(cfg_path)
+        tr = get_trainer_cls("rft")(c.train, c.wandb, c.model, rank, 0, ws)
+        tr.max_steps = 2
+        tr.train()
+        torch.cuda.synchronize()
+        q.put((rank, {k: p.detach().cpu().numpy() for k, p in tr.model.named_parameters()},
+               [s.detach().cpu().numpy() for s in tr.ema.shadow], tr.history))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trainer_two_ranks_on_gpu(tmp_path):
+    """The trainer's N > 1 path (rft_trainer.py:95-228) with 2 ranks sharing the card over gloo:
+    accum = target_batch / batch / world micro-steps per rank, the bucketed all-reduce, distributed
+    Muon, EMA, the eval sampler with n_samples split over ranks (rft_trainer.py:155-170), the logged
+    diffusion_loss summed over ranks (utils/logging.py:33-64), rank 0's checkpoint.  Replicas must be
+    bit-identical and log the same loss."""
+    import os as _os
+    import torch.multiprocessing as mp
+    c = _tiny_trainer_cfg(tmp_path, target_batch_size=4, sample_interval=2, sampler_id="av_caching", n_samples=2,
+                          sampler_kwargs={"n_steps": 2, "cfg_scale": 1.0, "num_frames": 2, "noise_prev": 0.2,
+                                          "only_return_generated": False},
+                          sample_data_id="cod", sample_data_kwargs={"window_length": 4})
+    assert c.train.target_batch_size == 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + _os.getpid() % 1000
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, str(tmp_path / "c.yml"))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (prm, ema, hist) for r, prm, ema, hist in (q.get(timeout=150) for _ in range(2))}
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (p0, e0, h0), (p1, e1, h1) = res[0], res[1]
+    assert p0.keys() == p1.keys()
+    for k in p0:
+        assert (p0[k] == p1[k]).all(), k
+    for a, b in zip(e0, e1):
+        assert (a == b).all()
+    assert len(h0) == len(h1) == 2
+    for r0, r1 in zip(h0, h1):
+        assert r0["diffusion_loss"] == r1["diffusion_loss"] and r0["step"] == r1["step"]
+        assert math.isfinite(r0["diffusion_loss"])
+    assert "eval/frames" in h0[0] and h0[0]["eval/samples"] == 2  # step 0 evaluates, 1 sample per rank
+    assert (tmp_path / "ckpt" / "step_2.pt").exists()
 
 
 def test_trainer_eval_sampler_at_sample_interval(tmp_path):
