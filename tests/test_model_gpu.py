@@ -648,6 +648,31 @@ def test_trainer_two_ranks_on_gpu(tmp_path):
     assert (tmp_path / "ckpt" / "step_2.pt").exists()
 
 
+def test_bench_two_ranks_json_line():
+    """bench.py's N > 1 path as the driver launches it (torch.distributed.run, 2 ranks, barrier +
+    max-over-ranks timing, one JSON line from rank 0), rehearsed with both ranks on this card
+    (OWL_BENCH_SHARE_GPU: collectives over gloo, since RCCL needs one GPU per rank) at 64 frames."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, OWL_BENCH_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
+    port = 29900 + os.getpid() % 97
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
+           "--warmup", "1", "--frames", "64", "--no-cpu-baseline", "--no-profile"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config"):
+        assert key in d, key
+    assert d["n_gpus"] == 2 and d["steps"] == 1 and d["warmup"] == 1 and d["value"] > 0
+    assert d["scaling"] == "strong" and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
+    assert abs(d["value"] - 16 * 64 * 64 / (d["ms_per_step"] / 1e3)) <= 1e-3 * d["value"]  # whole-job tokens / s
+
+
 def test_trainer_eval_sampler_at_sample_interval(tmp_path):
     """rft_trainer.py:213, 243-280: the EMA model's sampler runs at step 0 and every
     sample_interval; latents land in eval_sample_dir as vid.<step>.pt (4 context + 2 generated)."""
