@@ -104,6 +104,15 @@ int owlk_qk_rope_fwd_kv_dev(const void* qkv, long ldq, long T, long L, int H, in
 int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
                      const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
                      const float* rstd, void* dqkv, long ldg, void* stream);
+/* owlk_qk_rope_bwd with the column sums of its output fused: dbias[n] += sum_t bf16(dqkv[t, n]) for
+ * n < 2 H D -- the q / k part of the qkv Linear's bias gradient (attn.py:90; torch's Linear backward
+ * sums the bf16 output gradient over rows).  Per-token-block partials in ws (size from
+ * owlk_qk_rope_bwd_ws_bytes; 0 = shape not supported by the fused form), added in a fixed order. */
+long owlk_qk_rope_bwd_ws_bytes(long T, int H, int D);
+int owlk_qk_rope_bwd_bias(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
+                          const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
+                          const float* rstd, void* dqkv, long ldg, float* dbias, void* ws, long ws_bytes,
+                          void* stream);
 
 /* ---- Frame-masked flash attention (replaces compiled flex_attention + create_block_mask,
  *   attn.py:13-16,24-62,106-109; mmattn.py:75).  q/k/v/o token-major rows (head h at column

@@ -361,6 +361,71 @@ __global__ __launch_bounds__(256) void qk_rope_bwd_k(const bf16* __restrict__ dq
   *(bf16x8*)(dqkv + tok * ldg + (long)wh * D + j * 8) = pack8(o);
 }
 
+#ifndef OWLK_RB_UNROLL
+#define OWLK_RB_UNROLL 2
+#endif
+#ifndef OWLK_RB_MAXBLK
+#define OWLK_RB_MAXBLK 1024
+#endif
+// qk_rope_bwd_k with the column sums of its output fused (the q / k part of the qkv bias gradient,
+// attn.py:90's Linear bias): a workgroup is one row of 2 H D / 8 threads (8 columns each) walking
+// `rows_per` tokens, so every thread owns fixed columns and adds its bf16-rounded outputs; the
+// per-workgroup partial rows are summed in order by colsum_reduce (deterministic).  Saves the
+// separate colsum pass's re-read of the 2 H D columns (604 MB per dit_v4 layer).
+template <int D>
+__global__ __launch_bounds__(1024) void qk_rope_bwd_cs_k(const bf16* __restrict__ dqk, long ldd,
+                                                         const bf16* __restrict__ qkv, long ldq, long T, int H,
+                                                         const float* __restrict__ cosb,
+                                                         const float* __restrict__ sinb, long ld_tab, long tab_off,
+                                                         long tpos_div, const float* __restrict__ rstd,
+                                                         bf16* __restrict__ dqkv, long ldg, long rows_per,
+                                                         float* __restrict__ part) {
+  constexpr int CPR = D / 8;
+  const int wh = threadIdx.x / CPR, j = threadIdx.x % CPR;
+  const long N = 2L * H * D;
+  const long t0 = (long)blockIdx.x * rows_per, t1 = t0 + rows_per < T ? t0 + rows_per : T;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll OWLK_RB_UNROLL
+  for (long tok = t0; tok < t1; ++tok) {
+    const bf16* dp = dqk + tok * ldd + (long)wh * D;
+    const bf16x4 d0 = *(const bf16x4*)(dp + j * 4);
+    const bf16x4 d1 = *(const bf16x4*)(dp + D / 2 + j * 4);
+    const long pos = tab_off + (tpos_div > 0 ? tok % tpos_div : tok);
+    const f32x4 c = *(const f32x4*)(cosb + pos * ld_tab + j * 4);
+    const f32x4 s = *(const f32x4*)(sinb + pos * ld_tab + j * 4);
+    float dxn[8], xh[8], xv[8];
+    const float r = rstd[tok * 2 * H + wh];
+    unpack8(*(const bf16x8*)(qkv + tok * ldq + (long)wh * D + j * 8), xv);
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = (float)d0[i], b = (float)d1[i];
+      dxn[2 * i] = a * c[i] + b * s[i];
+      dxn[2 * i + 1] = b * c[i] - a * s[i];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xh[e] = xv[e] * r;
+      dot += dxn[e] * xh[e];
+    }
+#pragma unroll
+    for (int o = 1; o < CPR; o <<= 1) dot += __shfl_xor(dot, o, 64);
+    dot /= D;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = r * (dxn[e] - xh[e] * dot);
+    const bf16x8 ob = pack8(o);
+    *(bf16x8*)(dqkv + tok * ldg + (long)wh * D + j * 8) = ob;
+    float ov[8];
+    unpack8(ob, ov);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += ov[e];
+  }
+  float* dst = part + (long)blockIdx.x * N + (long)wh * D + j * 8;
+  *(f32x4*)dst = f32x4{cs[0], cs[1], cs[2], cs[3]};
+  *(f32x4*)(dst + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+}
+
 // ------------------------------------------------------------------ flow noise + patchify
 // x, z: [B, N, C, P] (P = h*w pixels); ts_raw: [B, N] fp32 (pre-sigmoid draw, bf16-valued)
 // out: xt_tok, tgt_tok: [B, N*P, C] bf16 token-major (gamerft.py:52 'b n c h w -> b (n h w) c')
@@ -634,6 +699,45 @@ extern "C" int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long
     hipLaunchKernelGGL(qk_rope_bwd_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)dqk, ldd,
                        (const bf16*)qkv, ldq, T, H, cosb, sinb, ld_tab, tab_off, tpos_div, rstd, (bf16*)dqkv, ldg);
   return owlk::check_launch("qk_rope_bwd");
+}
+
+// row-blocks of the fused-bias qk_rope backward: ~1024 workgroups, >= 16 tokens each; 0 = shape not
+// supported by the fused form (one row of 2 H D / 8 threads must be whole waves, <= 1024 threads)
+static long qk_rope_bwd_blocks(long T, int H, int D, long* rows_per) {
+  const long thr = 2L * H * D / 8;
+  if ((D != 64 && D != 128) || T <= 0 || thr % 64 || thr > 1024) return 0;
+  long nb = T / 16 < OWLK_RB_MAXBLK ? T / 16 : OWLK_RB_MAXBLK;
+  if (nb < 1) nb = 1;
+  const long rp = (T + nb - 1) / nb;
+  if (rows_per) *rows_per = rp;
+  return (T + rp - 1) / rp;
+}
+
+extern "C" long owlk_qk_rope_bwd_ws_bytes(long T, int H, int D) {
+  return qk_rope_bwd_blocks(T, H, D, nullptr) * 2L * H * D * (long)sizeof(float);
+}
+
+extern "C" int owlk_qk_rope_bwd_bias(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
+                                     const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
+                                     const float* rstd, void* dqkv, long ldg, float* dbias, void* ws, long ws_bytes,
+                                     void* stream) {
+  long rows_per = 0;
+  const long nb = qk_rope_bwd_blocks(T, H, D, &rows_per);
+  const long N = 2L * H * D;
+  OWLK_REQUIRE(nb > 0, "qk_rope_bwd_bias: H=%d D=%d not supported by the fused form", H, D);
+  OWLK_REQUIRE(ws && ws_bytes >= nb * N * (long)sizeof(float) && ((uintptr_t)ws & 15) == 0,
+               "qk_rope_bwd_bias: workspace too small or misaligned (owlk_qk_rope_bwd_ws_bytes)");
+  OWLK_REQUIRE(dbias && ((uintptr_t)dbias & 15) == 0, "qk_rope_bwd_bias: dbias must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((unsigned)nb), blk((unsigned)(N / 8));
+  if (D == 64)
+    hipLaunchKernelGGL(qk_rope_bwd_cs_k<64>, g, blk, 0, s, (const bf16*)dqk, ldd, (const bf16*)qkv, ldq, T, H, cosb,
+                       sinb, ld_tab, tab_off, tpos_div, rstd, (bf16*)dqkv, ldg, rows_per, (float*)ws);
+  else
+    hipLaunchKernelGGL(qk_rope_bwd_cs_k<128>, g, blk, 0, s, (const bf16*)dqk, ldd, (const bf16*)qkv, ldq, T, H, cosb,
+                       sinb, ld_tab, tab_off, tpos_div, rstd, (bf16*)dqkv, ldg, rows_per, (float*)ws);
+  if (int e = owlk::check_launch("qk_rope_bwd_bias")) return e;
+  return owlk::colsum_reduce((const float*)ws, (int)nb, N, dbias, s);
 }
 
 extern "C" int owlk_flow_noise(const void* x, const void* z, const float* ts_raw, int C, int P, long BN, void* xt,

@@ -28,6 +28,8 @@ _SIGS = {
     "owlk_qk_rope_fwd_kv_dev": [P, L, L, L, I, I, P, P, L, P, P, L, L, P, L, L, P, L, L, P],
     "owlk_attn_decode_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, I, F, F, P, L, L, P],
     "owlk_qk_rope_bwd": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P],
+    "owlk_qk_rope_bwd_ws_bytes": [L, I, I],
+    "owlk_qk_rope_bwd_bias": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P, P, L, P],
     "owlk_attn_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, L, I, F, F, L, I, I, L, P, P, P, P, L, P],
     "owlk_attn_delta": [P, P, L, L, L, I, I, P, P],
     "owlk_frame_mux": [I, L, I, I, I, P, L, P, L, P, L, P],
@@ -58,6 +60,7 @@ _SIGS = {
 
 # size queries; every other entry returns an int status
 _RESTYPES = {n: ctypes.c_long for n in ("owlk_gemm_splitk_bytes", "owlk_gemm_ws_bytes", "owlk_gemm_ws_counter_bytes",
+                                         "owlk_qk_rope_bwd_ws_bytes",
                                         "owlk_colsum_ws_bytes", "owlk_ns_iterate_ws_bytes",
                                         "owlk_newton_schulz_ws_bytes")}
 

@@ -199,10 +199,21 @@ def attn_decode_fwd(q, kbuf, vbuf, H, D, state, Lnew, window_tokens=0, scale=Non
     return o, lse
 
 
-def qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, dqkv, tab_off=0, tpos_div=0):
+def qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, dqkv, tab_off=0, tpos_div=0, dbias=None):
+    """-> dqkv[:, :2HD]; with dbias (fp32 [2HD]) also dbias += column sums of those outputs (the q / k
+    part of the qkv bias gradient), fused into the same pass where the shape allows."""
     T = qkv.shape[0]
-    call("owlk_qk_rope_bwd", ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin),
-         cos.stride(0), tab_off, tpos_div, ptr(rstd), ptr(dqkv), dqkv.stride(0), stream())
+    args = (ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin), cos.stride(0), tab_off,
+            tpos_div, ptr(rstd), ptr(dqkv), dqkv.stride(0))
+    nb = lib().owlk_qk_rope_bwd_ws_bytes(T, H, D) if dbias is not None else 0
+    if nb > 0:
+        assert dbias.dtype == F32 and dbias.is_contiguous() and dbias.numel() == 2 * H * D
+        ws = torch.empty(nb, device=qkv.device, dtype=torch.uint8)
+        call("owlk_qk_rope_bwd_bias", *args, ptr(dbias), ptr(ws), nb, stream())
+        return
+    call("owlk_qk_rope_bwd", *args, stream())
+    if dbias is not None:
+        colsum(dqkv[:, :2 * H * D], out=dbias)
 
 
 class FrameMask:

@@ -278,9 +278,15 @@ class DiTBlockFn(torch.autograd.Function):
         K.attn_bwd(q3, k3, qkv.view(B, T, 3 * d)[:, :, 2 * d:], o.view(B, T, d), do.view(B, T, d), lse, H, D,
                    geo.mask, dq3, dk3, dqkv.view(B, T, 3 * d)[:, :, 2 * d:])
         del do
-        K.qk_rope_bwd(dqkr, qkv, rq, H, D, geo.cos, geo.sin, dqkv, geo.tab_off, T)
+        # qkv bias gradient: the q / k columns' sums fused into the rope backward, the v columns' by colsum
+        sink_bqkv = grad_sink(prm[1])
+        dbqkv = sink_bqkv if sink_bqkv is not None else torch.zeros(3 * d, device=xx.device, dtype=torch.float32)
+        K.qk_rope_bwd(dqkr, qkv, rq, H, D, geo.cos, geo.sin, dqkv, geo.tab_off, T, dbias=dbqkv[:2 * d])
         del dqkr
-        dbqkv = bgrad_into(prm[1], dqkv)
+        K.colsum(dqkv[:, 2 * d:], out=dbqkv[2 * d:])
+        if sink_bqkv is not None:
+            grad_done(prm[1])
+            dbqkv = None
         dwqkv = wgrad_into(prm[0], dqkv, h1)
         dh1 = K.gemm(dqkv, bf16_weight(wqkv), b_trans=True)
         del dqkv

@@ -198,6 +198,26 @@ def test_qk_rope(D):
     assert rel(g, xf.grad) < 1e-2
 
 
+@pytest.mark.parametrize("D,H,T", [(64, 4, 1000), (128, 2, 777), (64, 24, 300)])
+def test_qk_rope_bwd_fused_bias(D, H, T):
+    """owlk_qk_rope_bwd_bias: the same dq / dk rows as owlk_qk_rope_bwd, bit for bit, and dbias +=
+    their column sums (the q / k part of the qkv bias gradient: sum over rows of the bf16 grads)."""
+    k = K()
+    ang = R.motion_rope_angles(4, 16, D)  # 1,024 positions >= T
+    cos, sin = ang.cos().to(DEV), ang.sin().to(DEV)
+    qkv = rnd(T, 3 * H * D, scale=2.0, seed=32)
+    _, rstd = k.qk_rope_fwd(qkv, H, D, cos, sin)
+    dqk = rnd(T, 2 * H * D, seed=33)
+    ref = torch.zeros(T, 3 * H * D, device=DEV, dtype=torch.bfloat16)
+    k.qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, ref)
+    got = torch.zeros_like(ref)
+    dbias = torch.ones(2 * H * D, device=DEV, dtype=torch.float32)  # added onto
+    k.qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, got, dbias=dbias)
+    assert torch.equal(got, ref)
+    want = ref[:, :2 * H * D].double().sum(0) + 1.0
+    assert ((dbias.double() - want).abs() <= 1e-5 * (want.abs() + 1.0)).all()
+
+
 ATTN_CASES = [
     # (B, H, n_frames, tpf, window, docs)
     (1, 2, 8, 64, None, False),
