@@ -96,6 +96,11 @@ def exported_symbols():
 _profile = None  # list of (key, flops, start_event, end_event) while a profile window is open
 
 
+def profiling():
+    """True while a profile window is open (its events time launches on the current stream)."""
+    return _profile is not None
+
+
 def profile_begin():
     global _profile
     _profile = []

@@ -3,11 +3,13 @@
 Every function checks shapes/strides on the host before the launch (a kernel never sees an
 operand its grid does not cover) and enqueues on torch's current HIP stream.
 """
+import ctypes
 import os
 
 import torch
 from torch.autograd.graph import increment_version
 
+from . import _lib
 from ._lib import call, lib, ptr, stream
 
 BF16, F32 = torch.bfloat16, torch.float32
@@ -300,6 +302,28 @@ def attn_fwd(q, k, v, H, D, mask, scale=None, o=None, score_bound=0.0):
     return o, lse
 
 
+_BWD_SIDE = {}
+
+
+def _bwd_side_stream(device, D, mask):
+    """A side stream for the dQ kernel, or None to run it after dK/dV on the caller's stream.
+    The two kernels are independent given delta (different outputs, shared read-only inputs).
+    Run side by side only where that measured faster (`tools/attn_bench.py --bwd-only`, same
+    process, interleaved; profiles/r2s_attn_bwd_side_stream.log): D 128 global layers, 20 heads x
+    98,304 tokens, 170.9 -> 161.8 ms (the one-wave-per-SIMD dK/dV leaves room for dQ workgroups).
+    D 64 global went 86.2 -> 89.1 ms and the window-16 layers moved within noise, so they stay
+    serial. OWLK_BWD_SIDE_STREAM=0 / 1 forces serial / side-by-side. Serial while a profile window
+    is open (its events time launches on the current stream) or a graph is being captured."""
+    env = os.environ.get("OWLK_BWD_SIDE_STREAM")
+    on = (D == 128 and mask.window is None) if env is None else env == "1"
+    if not on or _lib.profiling() or torch.cuda.is_current_stream_capturing():
+        return None
+    s = _BWD_SIDE.get(device)
+    if s is None:
+        s = _BWD_SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
 def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
     """Backward of attn_fwd (training shapes: Lq == Lkv, q_offset 0); all tensors [B, L, cols]."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
@@ -316,8 +340,18 @@ def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
             mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), *mask.args()[3:], stream())
     # algorithmic FLOPs: dV, dP, dK belong to the key-owner sweep, dQ to the other;
     # the dq kernel's recomputed S and dP are not counted
+    side = _bwd_side_stream(q.device, D, mask)
+    if side is not None:
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)  # delta and every input are ready
     call("owlk_attn_bwd_dkdv", *args, key=f"attn_bwd_dkdv[w{mask.window}]",
          flops=lambda: 6.0 * D * H * B * mask_pairs(mask, L, L))
+    if side is not None:
+        call("owlk_attn_bwd_dq", *args[:-1], ctypes.c_void_p(side.cuda_stream))
+        # joined before returning: later frees / reuses of these buffers on the caller's stream
+        # are ordered after the side stream's reads and writes
+        cur.wait_stream(side)
+        return
     call("owlk_attn_bwd_dq", *args, key=f"attn_bwd_dq[w{mask.window}]",
          flops=lambda: 2.0 * D * H * B * mask_pairs(mask, L, L))
 

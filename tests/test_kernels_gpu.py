@@ -277,6 +277,30 @@ def test_attention_fwd_bwd(case, D):
         assert rel(got.view(B, L, H, D).transpose(1, 2), ref) < 1e-2  # SURVEY §8(c) per-op
 
 
+@pytest.mark.parametrize("D,window", [(128, None), (64, None), (64, 16)])
+def test_attention_bwd_side_stream_equals_serial(D, window, monkeypatch):
+    """dQ on a side stream beside dK/dV (the default for D 128 global layers) gives the same bits
+    as the two kernels back to back on the caller's stream, and the caller's stream sees the
+    results without a host sync."""
+    k = K()
+    B, H, nf, tpf = 1, 4, 48, 64
+    L = nf * tpf
+    q, kk, v, do = (rnd(B * L, H * D, seed=s).view(B, L, H * D) for s in (50, 51, 52, 53))
+    mask = k.FrameMask(tpf, window)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("OWLK_BWD_SIDE_STREAM", mode)
+        assert (k._bwd_side_stream(q.device, D, mask) is not None) == (mode == "1")
+        g = [torch.full_like(q, float("nan")) for _ in range(3)]
+        k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, *g)
+        out[mode] = [t.clone() for t in g]  # on the caller's stream: ordered after the join
+    for a, b in zip(out["0"], out["1"]):
+        assert torch.equal(a, b)
+    monkeypatch.delenv("OWLK_BWD_SIDE_STREAM")
+    assert (k._bwd_side_stream(q.device, D, mask) is not None) == (D == 128 and window is None)
+
+
 @pytest.mark.parametrize("case,D", [(ATTN_CASES[0], 64), (ATTN_CASES[2], 64), (ATTN_CASES[4], 64), (ATTN_CASES[6], 64),
                                     (ATTN_CASES[2], 128)])
 def test_attention_fwd_score_bound(case, D):

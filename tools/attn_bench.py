@@ -65,7 +65,28 @@ def main():
             t_f0 = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o), args.iters)
         t_kv = timeit(lambda: _lib.call("owlk_attn_bwd_dkdv", *args_b), args.iters)
         t_q = timeit(lambda: _lib.call("owlk_attn_bwd_dq", *args_b), args.iters)
+        # dK/dV and dQ are independent given delta: the pair back to back on one stream against dQ
+        # on a side stream (fork / join by events), same process, interleaved
+        side = torch.cuda.Stream()
+        args_s = args_b[:-1] + (side.cuda_stream,)
+
+        def serial():
+            _lib.call("owlk_attn_bwd_dkdv", *args_b)
+            _lib.call("owlk_attn_bwd_dq", *args_b)
+
+        def concurrent():
+            side.wait_stream(torch.cuda.current_stream())
+            _lib.call("owlk_attn_bwd_dkdv", *args_b)
+            _lib.call("owlk_attn_bwd_dq", *args_s)
+            torch.cuda.current_stream().wait_stream(side)
+
+        t_ser, t_con = [], []
+        for _ in range(2):
+            t_ser.append(timeit(serial, args.iters))
+            t_con.append(timeit(concurrent, args.iters))
         print(f"window={window}: pairs/head={pairs / H:.4e}")
+        print(f"  bwd pair serial {min(t_ser):8.3f} ms, dQ on a side stream {min(t_con):8.3f} ms "
+              f"({t_ser} / {t_con})")
         print(f"  fwd   {t_f:8.3f} ms  {4 * D * pairs / t_f / 1e9:7.1f} TF/s (4 D pairs; fixed-offset softmax)")
         print(f"  fwd0  {t_f0:8.3f} ms  {4 * D * pairs / t_f0 / 1e9:7.1f} TF/s (running-max softmax)")
         print(f"  dkdv  {t_kv:8.3f} ms  {6 * D * pairs / t_kv / 1e9:7.1f} TF/s alg (6 D pairs; 8 D executed: "
