@@ -310,15 +310,15 @@ def _bwd_side_stream(device, D, mask):
     The two kernels are independent given delta (different outputs, shared read-only inputs).
     Run side by side only where that measured faster (`tools/attn_bench.py --bwd-only`, same
     process, interleaved; profiles/r2s_attn_bwd_side_stream.log): D 128 global layers, 20 heads x
-    98,304 tokens, 170.9 -> 161.8 ms (the one-wave-per-SIMD dK/dV leaves room for dQ workgroups);
-    D 64 windowed layers, 24 heads, window 16: 2.36 -> 2.33 ms (three interleaved rounds, 20
-    launches each). D 64 global layers went 86.2 -> 89.1 ms and D 128 windowed ones did not move,
-    so those stay serial. OWLK_BWD_SIDE_STREAM=0 / 1 forces serial / side-by-side. Serial while a
-    profile window is open (its events time launches on the current stream) or a graph is being
-    captured."""
+    98,304 tokens, 170.9 -> 161.8 ms (the one-wave-per-SIMD dK/dV leaves room for dQ workgroups).
+    D 64 global layers went 86.2 -> 89.1 ms and D 128 windowed ones did not move. D 64 window-16
+    layers gained in isolation (2.36 -> 2.33 ms) but the whole dit_v4 step lost 0.3 % with them
+    side by side (bench.py, two interleaved pairs, profiles/r2t_bench_side_stream_ab.log), so
+    everything but D 128 global stays serial. OWLK_BWD_SIDE_STREAM=0 / 1 forces serial /
+    side-by-side. Serial while a profile window is open (its events time launches on the current
+    stream) or a graph is being captured."""
     env = os.environ.get("OWLK_BWD_SIDE_STREAM")
-    default = (mask.window is None) if D == 128 else (mask.window is not None)
-    on = default if env is None else env == "1"
+    on = (D == 128 and mask.window is None) if env is None else env == "1"
     if not on or _lib.profiling() or torch.cuda.is_current_stream_capturing():
         return None
     s = _BWD_SIDE.get(device)
