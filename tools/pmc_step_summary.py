@@ -28,11 +28,11 @@ for f in glob.glob(d + "/**/p1_kernel_trace.csv", recursive=True):
 
 
 def family(n):
-    n = re.sub(r"\(.*", "", n)
-    n = re.sub(r"^void ", "", n).replace("(anonymous namespace)::", "")
-    if n.startswith("at::native") or "at::native" in n:
+    n = n.replace("(anonymous namespace)::", "")
+    if "at::native" in n:
         return "ATen"
-    return re.sub(r"<.*", "", n)
+    n = re.sub(r"^void ", "", re.sub(r"\(.*", "", n))
+    return re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", n)
 
 
 fam = defaultdict(lambda: [0.0, 0.0, 0.0, 0])  # busy, gui, ns, launches
