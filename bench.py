@@ -137,20 +137,37 @@ def pmc_traffic(args):
         except (subprocess.SubprocessError, OSError) as e:
             log(f"[bench] PMC pass {ctr} failed: {e}")
             return {}
+        rows = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 if r.get("Counter_Name") != ctr:
                     continue
                 for k, sym in PMC_KERNELS.items():
                     if re.search(sym, r.get("Kernel_Name", "")):
-                        vals.setdefault(k, {}).setdefault(ctr, []).append(float(r["Counter_Value"]) * 1024)
+                        rows.setdefault(k, []).append((int(r.get("Dispatch_Id", 0) or 0),
+                                                       float(r["Counter_Value"]) * 1024))
+        for k, rs in rows.items():  # launch order (dispatch id): the layer order of the micro-step
+            vals.setdefault(k, {})[ctr] = [v for _, v in sorted(rs)]
         shutil.rmtree(d, ignore_errors=True)
+    from owl_wms.configs import Config
+    mc = Config.from_yaml(os.path.join(REPO, args.config)).model
+    n_layers, every = mc.n_layers, getattr(mc, "local_idx", 4)
     out = {}
     for k, v in vals.items():
-        if len(v) == 2:
-            fetch = 2.0 * sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
-            write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"])
-            out[k] = {"bytes": fetch + write, "fetch": fetch, "write": write, "launches": len(v["FETCH_SIZE"])}
+        if len(v) == 2 and len(v["FETCH_SIZE"]) == len(v["WRITE_SIZE"]):
+            n = len(v["FETCH_SIZE"])
+            per = [2.0 * f + w for f, w in zip(v["FETCH_SIZE"], v["WRITE_SIZE"])]
+            fetch = 2.0 * sum(v["FETCH_SIZE"]) / n
+            write = sum(v["WRITE_SIZE"]) / n
+            out[k] = {"bytes": fetch + write, "fetch": fetch, "write": write, "launches": n}
+            if n == n_layers:
+                # one launch per layer: the forward runs layers 0..L-1, the backward L-1..0; layer i is
+                # global iff i % local_idx == 0 (attn.py:151-153) -- report the two layer kinds apart
+                layer = list(range(n)) if k == "attn_fwd" else list(range(n - 1, -1, -1))
+                for kind, want in (("global", True), ("local", False)):
+                    sel = [b for b, i in zip(per, layer) if (i % every == 0) == want]
+                    if sel:
+                        out[k][kind] = {"bytes": sum(sel) / len(sel), "launches": len(sel)}
     return out
 
 
@@ -332,8 +349,17 @@ def main():
             if tr:
                 roof["traffic"] = round(tr["bytes"])
                 roof["traffic_unit"] = "bytes/launch (HBM, PMC, this run)"
+                # algorithmic bytes of one launch (either layer kind): Q, K, V, dO in and dK, dV out
+                # (bf16 [T, H D] each) plus lse2 and delta (fp32 [H, T])
+                alg = tokens * mc.d_model * 2 * 6 + tokens * mc.n_heads * 4 * 2 if dom == "attn_bwd_dkdv" else None
                 roof["traffic_detail"] = {"fetch": round(tr["fetch"]), "write": round(tr["write"]),
                                           "launches": tr["launches"],
+                                          **{kind: {"bytes_per_launch": round(tr[kind]["bytes"]),
+                                                    "launches": tr[kind]["launches"],
+                                                    **({"x_algorithmic": round(tr[kind]["bytes"] / alg, 2)}
+                                                       if alg else {})}
+                                             for kind in ("global", "local") if kind in tr},
+                                          **({"algorithmic_bytes_per_launch": alg} if alg else {}),
                                           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
                                                     "one micro-step; FETCH_SIZE x2 (gfx950)"}
         if rank == 0:
@@ -361,6 +387,8 @@ def main():
                           "seq_len": tokens, "parallelism": f"dp{world}",
                           **({"docs_per_sample": args.docs} if args.docs > 1 else {})},
                "tokens_per_s_per_gpu": round(value / world, 1),
+               "value_is": "whole-job latent tokens/s over all ranks (the driver's bench contract: total "
+                           "tokens / max-over-ranks time); the per-GPU figure is tokens_per_s_per_gpu",
                "step_mfma_frac": round(value * (FLOP_PER_TOKEN if headline else fpt) / world / PEAK_BF16, 4),
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)

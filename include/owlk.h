@@ -116,7 +116,9 @@ int owlk_qk_rope_bwd_bias(const void* dqk, long ldd, const void* qkv, long ldq, 
 
 /* ---- Frame-masked flash attention (replaces compiled flex_attention + create_block_mask,
  *   attn.py:13-16,24-62,106-109; mmattn.py:75).  q/k/v/o token-major rows (head h at column
- *   h*head_dim), lse [B, H, Lq] natural-log.  Mask: frame = (token + q_offset) / tpf for queries,
+ *   h*head_dim).  lse [B, H, Lq] fp32 in BASE 2: lse2[q] = log2 sum_k exp(scale * q.k) over the
+ *   allowed keys (= the natural-log lse of flex_attention(..., return_lse=True) divided by ln 2;
+ *   -inf for a row with no allowed key).  The backward entries take it in this form.  Mask: frame = (token + q_offset) / tpf for queries,
  *   token / tpf for keys; causal; |fq - fk| < window (window <= 0: unlimited); doc[b, fq] ==
  *   doc[b, fk].  Frame helper arrays (int32 [B, n_frames], batch stride fstride, may be NULL
  *   without docs): kv_lo (first visible kv frame), q_hi (last query frame seeing a kv frame),
@@ -135,7 +137,8 @@ int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, lo
  * of Lq <= 64 queries per (batch, head), unmasked over [cache | Lnew new rows] of the cache
  * buffers kbuf / vbuf (the new rows written there first, owlk_qk_rope_fwd_kv_dev), or over the
  * last window_tokens of them (windowed layer; 0: all); state = {start, cached tokens, rope offset}
- * int64 on the device.  head_dim 64, bounded softmax (score_bound > 0) only. */
+ * int64 on the device.  head_dim 64 or 128, bounded softmax (score_bound > 0) only; lse base 2 as
+ * owlk_attn_fwd's. */
 int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const void* kbuf, long ldk, long skb,
                          const void* vbuf, long ldv, long svb, void* o, long ldo, long sob, float* lse, long B,
                          int H, long Lq, int head_dim, float scale, float score_bound, const long* state,

@@ -3,7 +3,7 @@
 // Replaces the compiled flex_attention + create_block_mask pair of the reference
 // (attn.py:13-16, 24-62, 106-109; mmattn.py:75).  Semantics: softmax(q k^T / sqrt(D)) v over the
 // allowed keys of attn_common.hpp, bf16 in / fp32 accumulate / bf16 out, plus the per-row
-// log-sum-exp (natural log) for the backward pass.
+// log-sum-exp in base 2 (lse2 = natural lse / ln 2, include/owlk.h) for the backward pass.
 //
 // Workgroup = 4 waves = 128 query rows of one (batch, head); each wave owns 32 rows.  Per 64-key
 // tile the wave computes S^T = K Q^T with v_mfma_f32_32x32x16_bf16 (key rows in registers, the
@@ -725,12 +725,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   }
 }
 
-// Decode form of attn_fwd16_k (D = 64, bounded softmax, no mask: one new frame of Lq <= 64 queries
-// against [cache | frame]).  A (batch, head) has a single 64-query block, so attn_fwd16_k would run
-// one wave per workgroup over every key tile in turn.  Here the 4 waves share the queries and split
-// the key tiles (wave w takes tiles w, w + 4, ...), each streaming its tiles by LDS-DMA into a
-// private 2-slot ring (no barriers in the sweep); with the bounded softmax (no running maximum)
-// the waves' partial O and row sums simply add, in wave order, through LDS at the end.
+// Decode form of attn_fwd16_k (bounded softmax, no mask: one new frame of Lq <= 64 queries against
+// [cache | frame]).  A (batch, head) has a single 64-query block, so attn_fwd16_k would run one wave per
+// workgroup over every key tile in turn.  Here the 4 waves share the queries and split the key tiles
+// (wave w takes tiles w, w + 4, ...), each streaming its tiles by LDS-DMA into a private 2-slot ring
+// (no barriers in the sweep); with the bounded softmax (no running maximum) the waves' partial O and
+// row sums simply add, in wave order, through LDS at the end.
+// D = 64: 64-key tiles (two 32-key halves).  D = 128: 32-key tiles, so the four private rings stay at
+// 4 x 2 x 16 KiB and the combine image [4][64][D + 4] fp32 (133 KiB) fits the 160 KiB LDS.
+template <int D>
+struct DecCfg {
+  static constexpr int KTD = D == 64 ? 64 : 32;  // keys per ring tile
+  static constexpr int NKC = KTD / 32;           // 32-key halves per tile
+  static constexpr int NSUB = D / 64;            // 64-column sub-tiles
+  static constexpr int SUBK = KTD * 128;         // bytes of one sub-tile (128-B rows)
+  static constexpr int TILEB = 2 * NSUB * SUBK;  // K sub-tiles | V sub-tiles
+  static constexpr int NKD = D / 32;             // k steps of S^T = K q'^T
+  static constexpr int NDS = D / 16;             // 16-column d tiles of O^T
+  static constexpr int OLD = D + 4;              // fp32 row stride of the combine image
+  static constexpr int RING = 2 * TILEB;         // per wave
+  static constexpr int COMB = 4 * 64 * OLD * 4 + 4 * 64 * 4;
+  static constexpr int SMEM = 4 * RING > COMB ? 4 * RING : COMB;
+  static constexpr int OPS = 2 * (KTD / 16) * 2 * NSUB;  // LDS-DMA wave-instructions per tile
+};
+
+template <int D>
 __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long* __restrict__ state, long Lnew,
                                                              long wtok) {
   // device-resident cache state (owlk_attn_decode_fwd): {start, cached tokens, rope offset} of the
@@ -743,27 +762,26 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
     p.v += (start + first) * p.ldv;
     p.Lkv = total - first;
   }
-  using C = Cfg<64>;
-  constexpr int RING = 2 * C::TILEB;  // per wave
-  constexpr int OLD = 68;             // fp32 row stride of the combine image
-  __shared__ __attribute__((aligned(16))) char smem[4 * RING];
+  using C = DecCfg<D>;
+  constexpr int KTD = C::KTD;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
   const long b = blockIdx.z;
   const int head = blockIdx.y;
-  const bf16* Q = p.q + b * p.sqb + head * 64;
-  const bf16* K = p.k + b * p.skb + head * 64;
-  const bf16* V = p.v + b * p.svb + head * 64;
-  const int ntiles = (int)((p.Lkv + KT - 1) / KT);
+  const bf16* Q = p.q + b * p.sqb + head * D;
+  const bf16* K = p.k + b * p.skb + head * D;
+  const bf16* V = p.v + b * p.svb + head * D;
+  const int ntiles = (int)((p.Lkv + KTD - 1) / KTD);
   const int nt = ntiles > w ? (ntiles - w + 3) / 4 : 0;  // this wave's tiles: w + 4 i
 
   int my_q[4];
-  bf16x8 qf[4][2];
+  bf16x8 qf[4][C::NKD];
 #pragma unroll
   for (int t4 = 0; t4 < 4; ++t4) {
     my_q[t4] = 16 * t4 + c;
 #pragma unroll
-    for (int kd = 0; kd < 2; ++kd) {
+    for (int kd = 0; kd < C::NKD; ++kd) {
       bf16x8 qv = my_q[t4] < p.Lq ? *(const bf16x8*)(Q + my_q[t4] * p.ldq + 32 * kd + 8 * g) : bf16x8{};
       float f[8];
       unpack8(qv, f);
@@ -772,46 +790,48 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
       qf[t4][kd] = pack8(f);
     }
   }
-  f32x4 o[4][4];
+  f32x4 o[C::NDS][4];
 #pragma unroll
-  for (int ds = 0; ds < 4; ++ds)
+  for (int ds = 0; ds < C::NDS; ++ds)
 #pragma unroll
     for (int t4 = 0; t4 < 4; ++t4) o[ds][t4] = f32x4{0.f, 0.f, 0.f, 0.f};
   float lrow[4] = {0.f, 0.f, 0.f, 0.f};
 
-  char* ring = smem + w * RING;
-  auto issue = [&](int i) {  // the wave's i-th tile (key tile w + 4 i), all 64 rows by this wave
-    const long c0 = (long)(w + 4 * i) * KT;
+  char* ring = smem + w * C::RING;
+  auto issue = [&](int i) {  // the wave's i-th tile (key tile w + 4 i), all KTD rows by this wave
+    const long c0 = (long)(w + 4 * i) * KTD;
     char* buf = ring + (i & 1) * C::TILEB;
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      tile_glds<SW_ROW>(buf, K, p.ldk, c0, p.Lkv, q4, lane);
-      tile_glds<SW_TR>(buf + SUB, V, p.ldv, c0, p.Lkv, q4, lane);
-    }
+    for (int sb = 0; sb < C::NSUB; ++sb)
+#pragma unroll
+      for (int q4 = 0; q4 < KTD / 16; ++q4) {
+        tile_glds<SW_ROW>(buf + sb * C::SUBK, K + 64 * sb, p.ldk, c0, p.Lkv, q4, lane);
+        tile_glds<SW_TR>(buf + (C::NSUB + sb) * C::SUBK, V + 64 * sb, p.ldv, c0, p.Lkv, q4, lane);
+      }
   };
   if (nt > 0) issue(0);
   if (nt > 1) issue(1);
   for (int i = 0; i < nt; ++i) {
     if (i + 1 < nt)
-      vmcnt<16>();  // tile i landed (this wave's own DMA: no barrier), i + 1 in flight
+      vmcnt<C::OPS>();  // tile i landed (this wave's own DMA: no barrier), i + 1 in flight
     else
       vmcnt<0>();
-    const long c0 = (long)(w + 4 * i) * KT;
+    const long c0 = (long)(w + 4 * i) * KTD;
     const char* lk = ring + (i & 1) * C::TILEB;
-    const char* lv = lk + SUB;
-    const bool ragged = c0 + KT > p.Lkv;
+    const char* lv = lk + C::NSUB * C::SUBK;
+    const bool ragged = c0 + KTD > p.Lkv;
 #pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
+    for (int kc = 0; kc < C::NKC; ++kc) {
       f32x4 st[2][4];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4) st[kk][t4] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kd = 0; kd < 2; ++kd)
+      for (int kd = 0; kd < C::NKD; ++kd)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 ak = frag_row16<SW_ROW>(lk, 32 * kc + 16 * kk, kd, lane);
+          const bf16x8 ak = frag_row16<SW_ROW>(lk + (kd >> 1) * C::SUBK, 32 * kc + 16 * kk, kd & 1, lane);
 #pragma unroll
           for (int t4 = 0; t4 < 4; ++t4)
             st[kk][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t4][kd], st[kk][t4], 0, 0, 0);
@@ -846,8 +866,8 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
         pf[t4] = pack_perm(st[0][t4], st[1][t4]);
       }
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        const bf16x8 vt = frag_tr16<SW_TR>(lv, 32 * kc, ds, lane);
+      for (int ds = 0; ds < C::NDS; ++ds) {
+        const bf16x8 vt = frag_tr16<SW_TR>(lv + (ds >> 2) * C::SUBK, 32 * kc, ds & 3, lane);
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4)
           o[ds][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pf[t4], o[ds][t4], 0, 0, 0);
@@ -860,16 +880,17 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
     }
   }
   // combine: wave partials (O^T tiles: d = 16 ds + 4 g + r, query 16 t4 + c) -> LDS [w][q][d], then
-  // each thread sums one query's 16 columns over the 4 waves in order
+  // each thread sums D / 4 columns of one query over the 4 waves in order
   vmcnt<0>();
   __syncthreads();
-  float* img = (float*)smem;                      // [4][64][OLD]
-  float* lsum = (float*)(smem + 4 * 64 * OLD * 4);  // [4][64]
+  constexpr int OLD = C::OLD;
+  float* img = (float*)smem;                          // [4][64][OLD]
+  float* lsum = (float*)(smem + 4 * 64 * OLD * 4);    // [4][64]
 #pragma unroll
   for (int t4 = 0; t4 < 4; ++t4) {
     const int q = 16 * t4 + c;
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds)
+    for (int ds = 0; ds < C::NDS; ++ds)
 #pragma unroll
       for (int r = 0; r < 4; ++r) img[(w * 64 + q) * OLD + 16 * ds + 4 * g + r] = o[ds][t4][r];
     float lt = lrow[t4] + __shfl_xor(lrow[t4], 16, 64);
@@ -877,15 +898,16 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
     if (g == 0) lsum[w * 64 + q] = lt;
   }
   __syncthreads();
-  const int q = threadIdx.x >> 2, d0 = 16 * (threadIdx.x & 3);
+  constexpr int DQ = D / 4;  // columns per thread
+  const int q = threadIdx.x >> 2, d0 = DQ * (threadIdx.x & 3);
   if (q >= p.Lq) return;
   float l = 0.f;
 #pragma unroll
   for (int ww = 0; ww < 4; ++ww) l += lsum[ww * 64 + q];
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16* O = p.o + b * p.sob + (long)q * p.ldo + head * 64 + d0;
+  bf16* O = p.o + b * p.sob + (long)q * p.ldo + head * D + d0;
 #pragma unroll
-  for (int h8 = 0; h8 < 2; ++h8) {
+  for (int h8 = 0; h8 < DQ / 8; ++h8) {
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = 0.f;
@@ -908,10 +930,10 @@ void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   // decode: one unmasked <= 64-query block per (batch, head) over >= 4 key tiles
   static const int split = getenv("OWLK_FWD_SPLIT") ? atoi(getenv("OWLK_FWD_SPLIT")) : 1;
   const MaskP& m = p.m;
-  if (D == 64 && split && p.bound > 0.f && p.Lq <= 64 && p.Lkv >= 4 * KT && m.window == 0 && !m.causal &&
-      !m.kv_lo && !m.doc && m.q_offset == 0) {
-    hipLaunchKernelGGL(attn_fwd16_split_k, dim3(1, grid.y, grid.z), dim3(256), 0, s, p, (const long*)nullptr, 0L,
-                       0L);
+  if (split && p.bound > 0.f && p.Lq <= 64 && p.Lkv >= 4 * KT && m.window == 0 && !m.causal && !m.kv_lo &&
+      !m.doc && m.q_offset == 0) {
+    hipLaunchKernelGGL(attn_fwd16_split_k<D>, dim3(1, grid.y, grid.z), dim3(256), 0, s, p, (const long*)nullptr,
+                       0L, 0L);
     return;
   }
   if (D == 64 && f16 && p.bound > 0.f) {
@@ -988,7 +1010,7 @@ extern "C" int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const voi
                                     const void* vbuf, long ldv, long svb, void* o, long ldo, long sob, float* lse,
                                     long B, int H, long Lq, int head_dim, float scale, float score_bound,
                                     const long* state, long Lnew, long window_tokens, void* stream) {
-  OWLK_REQUIRE(head_dim == 64, "attn_decode_fwd: head_dim %d not built (64)", head_dim);
+  OWLK_REQUIRE(head_dim == 64 || head_dim == 128, "attn_decode_fwd: head_dim %d not built (64, 128)", head_dim);
   OWLK_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lq <= 64 && Lnew > 0 && state, "attn_decode_fwd: bad sizes");
   OWLK_REQUIRE(score_bound > 0.f && score_bound * scale < 40.f, "attn_decode_fwd: needs a score bound");
   OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)kbuf | (uintptr_t)vbuf | (uintptr_t)o) % 16 == 0 && ldq % 8 == 0 &&
@@ -1002,7 +1024,11 @@ extern "C" int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const voi
   p.scale_log2 = scale * LOG2E;
   p.bound = score_bound;
   p.m = owlk_make_mask(1, 0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, 0);
-  hipLaunchKernelGGL(attn_fwd16_split_k, dim3(1, (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream, p,
-                     state, Lnew, window_tokens);
+  if (head_dim == 64)
+    hipLaunchKernelGGL(attn_fwd16_split_k<64>, dim3(1, (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                       p, state, Lnew, window_tokens);
+  else
+    hipLaunchKernelGGL(attn_fwd16_split_k<128>, dim3(1, (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
+                       p, state, Lnew, window_tokens);
   return owlk::check_launch("attn_decode_fwd");
 }

@@ -75,6 +75,7 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
 
 
 _DECODE_WS = {}
+_DECODE_WS_RETIRED = []  # replaced decode workspaces (zeroed counters), kept for captured graphs
 
 
 def _decode_ws(device, nbytes):
@@ -90,6 +91,10 @@ def _decode_ws(device, nbytes):
         fresh = torch.zeros(max(nbytes, 1 << 20), device=device, dtype=torch.uint8)
         if torch.cuda.is_current_stream_capturing():
             return fresh
+        if buf is not None:
+            # a HIP graph captured earlier may still hold the old buffer's address (the samplers'
+            # step graph outlives eager forwards between replays): keep it alive, never free it
+            _DECODE_WS_RETIRED.append(buf)
         _DECODE_WS[key] = buf = fresh
     return buf
 
@@ -187,11 +192,17 @@ def qk_rope_fwd_kv_dev(qkv, B, L, H, D, cos, sin, state, q_out, kbuf, vbuf):
          ptr(vbuf), vbuf.stride(1), vbuf.stride(0), stream())
 
 
+def decode_dev_supported(D, L):
+    """owlk_attn_decode_fwd's shapes: head_dim 64 or 128, one frame of at most 64 query rows."""
+    return D in (64, 128) and 0 < L <= 64
+
+
 def attn_decode_fwd(q, kbuf, vbuf, H, D, state, Lnew, window_tokens=0, scale=None, score_bound=0.0):
     """Decode attention over the cache buffers with the cache position on the device (state, see
     qk_rope_fwd_kv_dev): q [B, Lq <= 64, H D] against [cache | Lnew new rows] (or its last
     window_tokens rows) -> o [B, Lq, H D], lse [B, H, Lq] (base 2)."""
     B, Lq, _ = q.shape
+    assert decode_dev_supported(D, Lq), f"attn_decode_fwd: head_dim {D} / {Lq} query rows not supported"
     o = torch.empty_like(q)
     lse = torch.empty(B, H, Lq, device=q.device, dtype=F32)
     call("owlk_attn_decode_fwd", ptr(q), q.stride(1), q.stride(0), ptr(kbuf), kbuf.stride(1), kbuf.stride(0),

@@ -94,7 +94,8 @@ class Attn(nn.Module):
         H = self.n_heads
         D = d // H
         offset = kv_cache.get_offset(self.layer_idx) if kv_cache is not None else 0
-        if block_mask is None and getattr(kv_cache, "dev", None) is not None and offset > 0:
+        if block_mask is None and getattr(kv_cache, "dev", None) is not None and offset > 0 and \
+                K.decode_dev_supported(D, L):
             # decode with the cache position on the device (one captured graph for every frame)
             kb, vb = kv_cache.bufs[self.layer_idx]
             q = torch.empty(B, L, d, device=qkv.device, dtype=torch.bfloat16)

@@ -15,6 +15,7 @@ the keys the reference's forward sees.
 """
 import torch
 
+from .. import kernels as K
 from ..nn.kv_cache import KVCache
 from .schedulers import get_deltas, get_sd3_euler
 
@@ -151,7 +152,9 @@ class AVCachingSamplerV2:
         self._step_graph = None
         # the cache position on the device (one captured step for every frame); the same kernels run
         # in eager mode too, so eager and graphed decode stay bit-identical
-        dev_state = self.device_state and hasattr(kv_cache, "enable_device_state")
+        cfgm = model.config
+        dev_state = self.device_state and hasattr(kv_cache, "enable_device_state") and \
+            K.decode_dev_supported(cfgm.d_model // cfgm.n_heads, cfgm.tokens_per_frame)
         if dev_state:  # room for every frame up front: fixed buffer addresses for the one graph
             kv_cache.enable_device_state((init_len + num_frames + 1) * model.config.tokens_per_frame)
         model.transformer.enable_decoding()

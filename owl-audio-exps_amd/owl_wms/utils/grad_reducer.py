@@ -73,8 +73,13 @@ class GradReducer:
                 p.grad = p._owl_grad_view
 
     def grad_ready(self, p):
-        """p's gradient for this micro-step is complete in its bucket view (autograd's
-        post-accumulate hook, or a direct write by the fused backward)."""
+        """p's gradient for this micro-step is complete in its bucket view (a direct write by the
+        fused backward).  The direct writes assume one use of p per forward: a second write on the
+        synchronising micro-step would land in a bucket whose async all-reduce may already run."""
+        if self.sync and p in self.ready:
+            raise RuntimeError("GradReducer: a parameter's gradient was written twice in the synchronising "
+                               "micro-step (parameter used twice per forward?); its bucket may already be "
+                               "in flight")
         self._hook(p)
 
     def _hook(self, p):

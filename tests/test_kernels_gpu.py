@@ -327,14 +327,15 @@ def test_attention_fwd_score_bound(case, D):
     assert rel(o, o0) < 5e-3
 
 
+@pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("Lq,Lkv", [(64, 256), (64, 640), (37, 1000), (64, 4096), (1, 320)])
-def test_attention_decode_split_keys(Lq, Lkv):
+def test_attention_decode_split_keys(Lq, Lkv, D):
     """Decode attention (one frame of <= 64 queries, unmasked over [cache | frame], bounded
     softmax): the 4 waves of a workgroup split the key tiles and add their partial O / row sums.
     == oracle (rel 1e-2); lse within 4e-3 of the single-wave kernel (OWLK_FWD_SPLIT=0 path is the
-    one every other test covers); deterministic."""
+    one every other test covers); deterministic.  D 128 (dit_v4_5B) sweeps 32-key tiles."""
     k = K()
-    B, H, D = 2, 3, 64
+    B, H = 2, 3
     unit = lambda t, L: (t.float().view(-1, H, D) * torch.rsqrt(t.float().view(-1, H, D).pow(2).mean(-1, keepdim=True))
                          ).bfloat16().view(B, L, H * D)
     q = unit(rnd(B * Lq, H * D, seed=70), Lq)
@@ -350,6 +351,67 @@ def test_attention_decode_split_keys(Lq, Lkv):
     assert rel(o, o0) < 5e-3
     o2, lse2 = k.attn_fwd(q, kk, v, H, D, mask, score_bound=k.qk_norm_bound(D))
     assert torch.equal(o, o2) and torch.equal(lse, lse2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("Lq,start,cached,window", [(64, 0, 576, 0), (64, 128, 960, 256), (50, 64, 200, 0),
+                                                     (64, 0, 64, 128)])
+def test_attention_decode_device_state(D, Lq, start, cached, window):
+    """owlk_attn_decode_fwd (the cache position read from the device: {start, cached, offset}) over
+    cache buffers with rows [start, start + cached + Lq) live == attn_fwd on the same keys as explicit
+    views (the last `window` of them for a windowed layer), within the two kernels' summation order."""
+    k = K()
+    B, H, cap = 2, 2, 2048
+    unit = lambda t: (t.float().view(*t.shape[:-1], H, D) * torch.rsqrt(
+        t.float().view(*t.shape[:-1], H, D).pow(2).mean(-1, keepdim=True))).bfloat16().view(t.shape)
+    q = unit(rnd(B, Lq, H * D, seed=80))
+    kb = unit(rnd(B, cap, H * D, seed=81))
+    vb = rnd(B, cap, H * D, seed=82)
+    state = torch.tensor([start, cached, 0, 0], dtype=torch.int64, device=DEV)
+    o, lse = k.attn_decode_fwd(q, kb, vb, H, D, state, Lq, window, score_bound=k.qk_norm_bound(D))
+    total = cached + Lq
+    first = total - window if 0 < window < total else 0
+    ks, vs = kb[:, start + first:start + total], vb[:, start + first:start + total]
+    o_ref, lse_ref = k.attn_fwd(q, ks, vs, H, D, k.FrameMask(1, None, False, 0, None), score_bound=k.qk_norm_bound(D))
+    assert rel(o, o_ref) < 5e-3
+    assert (lse - lse_ref).abs().max().item() < 4e-3
+
+
+@pytest.mark.parametrize("D,window", [(64, None), (64, 2), (128, None)])
+def test_integration_binding_lse_contract(D, window):
+    """The reference-side binding of INTEGRATION.md (owlk_bind.attn_fwd) run against the real
+    libowlk.so: o == oracle attention, and lse2 is what include/owlk.h documents -- BASE 2,
+    lse2 * ln 2 == torch.logsumexp(scale * q k^T) over the allowed keys (flex_attention's
+    return_lse), on the frame mask of attn.py:24-62."""
+    import math
+    import os
+    import re
+    from conftest import REPO
+    from owl_wms._lib import LIB_PATH, lib
+    lib()  # torch's HIP runtime first, then the library (as the binding's comment says)
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = [b for b in re.findall(r"```python\n(.*?)```", text, flags=re.S) if "ctypes.CDLL" in b][0]
+    old = os.environ.get("OWLK_LIB")
+    os.environ["OWLK_LIB"] = LIB_PATH
+    try:
+        ns = {}
+        exec(compile(block, "INTEGRATION.md", "exec"), ns)
+    finally:
+        if old is None:
+            os.environ.pop("OWLK_LIB")
+        else:
+            os.environ["OWLK_LIB"] = old
+    B, H, nf, tpf = 2, 2, 6, 64
+    L = nf * tpf
+    q, kk, v = (rnd(B, L, H, D, seed=s) for s in (90, 91, 92))
+    o, lse2 = ns["attn_fwd"](q, kk, v, tpf, window)
+    torch.cuda.synchronize()
+    qr, kr, vr = (t.cpu().float().transpose(1, 2) for t in (q, kk, v))
+    m = R.frame_mask(L, L, tpf, window, None)
+    assert rel(o.transpose(1, 2), R.attention(qr, kr, vr, m)) < 1e-2
+    sc = (qr @ kr.transpose(-1, -2)) * D ** -0.5
+    lse_nat = torch.logsumexp(sc.masked_fill(~m[:, None], float("-inf")), -1)
+    assert (lse2.cpu() * math.log(2.0) - lse_nat).abs().max().item() < 2e-2
 
 
 def test_attention_dit_v4_shape_smoke():
@@ -375,17 +437,22 @@ def _sample_rows(L, tpf, n, seed):
     return torch.tensor(sorted(set(fixed + extra)), device=DEV)
 
 
+@pytest.mark.parametrize("H,D", [(24, 64), (20, 128)])
 @pytest.mark.parametrize("window", [None, 16])
-def test_attention_bwd_dit_v4_shape_sampled_rows(window):
+def test_attention_bwd_dit_v4_shape_sampled_rows(window, H, D):
     """The production shape (B 1 x H 24 x 98,304 tokens, tpf 64, global and window-16 layers, the
     QK-RMSNorm'd inputs and score_bound of the model; attn.py:24-62, 106-109) through owlk_attn_fwd
     and the two backward kernels -- every block of the XCD-aware remap and the 128-row tile paths
     run as in the bench -- checked on sampled rows of four heads against fp32 torch: O and dQ of
     sampled query rows over all their allowed keys; dK and dV of sampled key rows over all their
     allowed queries (with fp32 lse and delta recomputed for every query of the head).  Tolerance:
-    rel-L2 <= 1e-2 (SURVEY §8(c) per-op) over the sampled rows."""
+    rel-L2 <= 1e-2 (SURVEY §8(c) per-op) over the sampled rows.  H 20 x D 128 is dit_v4_5B's shape
+    (configs/dit_v4_5B.yml: d 2560 / 20 heads); its global layers run dQ on the side stream beside
+    dK/dV (the default, kernels._bwd_side_stream)."""
     k = K()
-    B, H, nf, tpf, D = 1, 24, 1536, 64, 64
+    B, nf, tpf = 1, 1536, 64
+    if D == 128 and window is None:
+        assert k._bwd_side_stream(torch.device(DEV), D, k.FrameMask(tpf, window)) is not None
     L = nf * tpf
     gen = torch.Generator(device=DEV).manual_seed(11)
 
@@ -417,7 +484,7 @@ def test_attention_bwd_dit_v4_shape_sampled_rows(window):
 
     qrows, krows = _sample_rows(L, tpf, 16, 1), _sample_rows(L, tpf, 16, 2)
     got, ref = {n: [] for n in ("o", "dq", "dk", "dv")}, {n: [] for n in ("o", "dq", "dk", "dv")}
-    for h in (0, 7, 13, 23):
+    for h in (0, 7, 13, H - 1):
         cs = slice(h * D, (h + 1) * D)
         qh, kh, vh, doh = (t[0, :, cs].float() for t in (q, kk, v, do))
         lse_r = torch.empty(L, device=DEV)

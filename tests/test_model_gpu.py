@@ -36,10 +36,13 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _model():
+def _model(d_model=128):
+    """TINY (d128 / 2 heads: head_dim 64); d_model=256 gives head_dim 128 (the dit_v4_5B attention
+    shape) with the gamerft_d128 fixture's weights."""
     from owl_wms.configs import model_config
     from owl_wms.models.gamerft import GameRFT
-    return det_init_(GameRFT(model_config(**TINY)), base_seed=1000).cuda().train()
+    return det_init_(GameRFT(model_config(**dict(TINY, d_model=d_model))),
+                     base_seed=1000 if d_model == 128 else 1100).cuda().train()
 
 
 def _run(mode="bf16"):
@@ -181,10 +184,12 @@ def test_audio_config1_trajectory():
         assert abs(loss.item() - ref[step].item()) / ref[step].item() < 2e-2, (step, loss.item(), ref[step].item())
 
 
-def test_kv_cache_decode_matches_full_forward():
-    """SURVEY §4 invariant: cached decode of the last frame == the full masked forward."""
+@pytest.mark.parametrize("d_model", [128, 256])
+def test_kv_cache_decode_matches_full_forward(d_model):
+    """SURVEY §4 invariant: cached decode of the last frame == the full masked forward (head_dim 64
+    and, at d_model 256, 128: the dit_v4_5B eval path, attn.py:86-107)."""
     from owl_wms.nn.kv_cache import KVCache
-    m = _model().eval()
+    m = _model(d_model).eval()
     core = m.core
     B, n = 1, 8
     x = det_tensor((B, n, 32, 8, 8), 900).cuda()
@@ -425,13 +430,15 @@ def test_trainer_reads_packed_table(tmp_path):
     assert all(torch.isfinite(torch.tensor(h["diffusion_loss"])) for h in tr.history)
 
 
-@pytest.mark.parametrize("n_steps,cfg,custom", [(4, 1.3, None), (3, 1.0, None), (3, 1.3, [1.0, 0.7, 0.3])])
-def test_graphed_decode_equals_eager(n_steps, cfg, custom):
+@pytest.mark.parametrize("n_steps,cfg,custom,d_model", [(4, 1.3, None, 128), (3, 1.0, None, 128),
+                                                       (3, 1.3, [1.0, 0.7, 0.3], 128), (3, 1.3, None, 256)])
+def test_graphed_decode_equals_eager(n_steps, cfg, custom, d_model):
     """compile_on_decode: the per-frame Euler steps replayed from a HIP graph give the same sampled
     latents as the eager loop, bit for bit (same kernels, same buffers' contents, same order);
-    also with a custom schedule (its deltas live in device memory the graph reads)."""
+    also with a custom schedule (its deltas live in device memory the graph reads) and at head_dim
+    128 (d_model 256: dit_v4_5B's decode shape)."""
     from owl_wms.sampling import get_sampler_cls
-    m = _model().eval()
+    m = _model(d_model).eval()
     g = torch.Generator().manual_seed(5)
     x = torch.randn(2, 4, 32, 8, 8, generator=g).bfloat16().cuda()
     mouse = torch.randn(2, 8, 2, generator=g).bfloat16().cuda()
@@ -446,13 +453,15 @@ def test_graphed_decode_equals_eager(n_steps, cfg, custom):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_device_state_decode_matches_host_state():
+@pytest.mark.parametrize("d_model", [128, 256])
+def test_device_state_decode_matches_host_state(d_model):
     """AVCachingSamplerV2 with the cache position on the device (owlk_qk_rope_fwd_kv_dev +
     owlk_attn_decode_fwd: one captured step for every frame) == the host-position decode path
     (lengths baked into each launch), eager, within attention summation order; the graphed
-    device-state run equals its eager run bit for bit (test_graphed_decode_equals_eager)."""
+    device-state run equals its eager run bit for bit (test_graphed_decode_equals_eager).
+    d_model 256 = head_dim 128 (dit_v4_5B)."""
     from owl_wms.sampling import get_sampler_cls
-    m = _model().eval()
+    m = _model(d_model).eval()
     g = torch.Generator().manual_seed(7)
     x = torch.randn(2, 4, 32, 8, 8, generator=g).bfloat16().cuda()
     mouse = torch.randn(2, 9, 2, generator=g).bfloat16().cuda()
@@ -518,7 +527,7 @@ def test_data_parallel_step_two_ranks_on_gpu():
         assert (res[0][k] == res[1][k]).all(), k
 
 
-def _tiny_trainer_cfg(tmp_path, **train_over):
+def _tiny_trainer_cfg(tmp_path, model_over=None, **train_over):
     import yaml
     from owl_wms.configs import Config
     train = {"trainer_id": "rft", "data_id": "synthetic", "data_kwargs": {"window_length": 8},
@@ -527,7 +536,7 @@ def _tiny_trainer_cfg(tmp_path, **train_over):
              "checkpoint_dir": str(tmp_path / "ckpt"), "save_interval": 2, "sample_interval": 10 ** 9,
              "vae_scale": 1.0, "seed": 77}
     train.update(train_over)
-    (tmp_path / "c.yml").write_text(yaml.safe_dump({"model": dict(TINY), "train": train,
+    (tmp_path / "c.yml").write_text(yaml.safe_dump({"model": dict(TINY, **(model_over or {})), "train": train,
                                                     "wandb": {"project": "p", "run_name": "r"}}))
     return Config.from_yaml(str(tmp_path / "c.yml"))
 
@@ -670,7 +679,11 @@ def test_bench_two_ranks_json_line():
         assert key in d, key
     assert d["n_gpus"] == 2 and d["steps"] == 1 and d["warmup"] == 1 and d["value"] > 0
     assert d["scaling"] == "strong" and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
-    assert abs(d["value"] - 16 * 64 * 64 / (d["ms_per_step"] / 1e3)) <= 1e-3 * d["value"]  # whole-job tokens / s
+    # value: whole-job tokens / s (the driver's contract: total over all ranks / max-over-ranks time,
+    # it computes scaling efficiency from the per-N values itself); the metric's per-GPU reading is
+    # tokens_per_s_per_gpu = value / n_gpus
+    assert abs(d["value"] - 16 * 64 * 64 / (d["ms_per_step"] / 1e3)) <= 1e-3 * d["value"]
+    assert abs(d["tokens_per_s_per_gpu"] - d["value"] / d["n_gpus"]) <= 0.1
 
 
 def test_trainer_eval_sampler_at_sample_interval(tmp_path):
@@ -689,6 +702,28 @@ def test_trainer_eval_sampler_at_sample_interval(tmp_path):
     for step in (0, 2):
         v = torch.load(tmp_path / "eval" / f"vid.{step}.pt", weights_only=True)
         assert v.shape == (1, 6, 32, 8, 8) and torch.isfinite(v.float()).all()
+
+
+def test_trainer_eval_sampler_head_dim_128(tmp_path):
+    """dit_v4_5B's eval path at head_dim 128 (d 256 / 2 heads): the trainer evaluates with the
+    av_caching sampler (device-state decode, graphed Euler steps) at step 0 and every step
+    (sample_interval 1) of a 2-step Muon run (configs/dit_v4_5B.yml sampler_id av_caching;
+    rft_trainer.py:213, 243-280)."""
+    from owl_wms.trainers import get_trainer_cls
+    c = _tiny_trainer_cfg(tmp_path, model_over={"d_model": 256, "gradient_checkpointing": True}, sample_interval=1,
+                          sampler_id="av_caching", n_samples=1,
+                          sampler_kwargs={"n_steps": 3, "cfg_scale": 1.3, "num_frames": 3, "noise_prev": 0.2,
+                                          "only_return_generated": False},
+                          sample_data_id="cod", sample_data_kwargs={"window_length": 4},
+                          eval_sample_dir=str(tmp_path / "eval"))
+    tr = get_trainer_cls("rft")(c.train, c.wandb, c.model, 0, 0, 1)
+    assert tr.model.core.transformer.blocks[0].attn.qkv.weight.shape[1] // c.model.n_heads == 128
+    tr.max_steps = 2
+    tr.train()
+    assert [("eval/frames" in h) for h in tr.history] == [True, True]
+    for step in (0, 1):
+        v = torch.load(tmp_path / "eval" / f"vid.{step}.pt", weights_only=True)
+        assert v.shape == (1, 7, 32, 8, 8) and torch.isfinite(v.float()).all()
 
 
 def test_optimizer_step_refreshes_bf16_weights():
