@@ -800,11 +800,13 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
 // 32-key block two 16-row key tiles; S and dP take K / V rows from LDS as A and q' = bf16(c q) /
 // dO from registers as B, so their accumulators (key on rows 4 g + r) are the B operands of
 // dQ^T += K^T dS in the permuted key order, K^T read by two ds_read_b64_tr_b16 per fragment.
-template <int QT>
+// D 128 (dit_v4_5B): two 64-column LDS sub-tiles per K / V tile, QT = 1 with a two-slot ring
+// (64 KiB per workgroup, two workgroups per CU).
+template <int D, int QT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
-  constexpr int D = 64;
-  constexpr int NBUF = QT == 2 ? 2 : Cfg<D>::NBUF, TLK = TL * QT;
-  constexpr int BUF = 2 * QT * SUB;  // K [QT] | V [QT]
+  constexpr int NSUB = D / 64, NKD = D / 32, NDS = D / 16;
+  constexpr int NBUF = (QT == 2 || D == 128) ? 2 : Cfg<D>::NBUF, TLK = TL * QT;
+  constexpr int BUF = 2 * QT * NSUB * SUB;  // K [QT][NSUB] | V [QT][NSUB]
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + 16];
   int& red_lo = *(int*)(smem + NBUF * BUF);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -844,14 +846,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
 
   long my_q[2];
   bool qok[2];
-  bf16x8 qf[2][2], df[2][2];  // [query tile][k step of 32 d]
+  bf16x8 qf[2][NKD], df[2][NKD];  // [query tile][k step of 32 d]
   f32x4 sinit[2], pinit[2];
 #pragma unroll
   for (int t2 = 0; t2 < 2; ++t2) {
     my_q[t2] = r0 + 16 * t2 + c;
     qok[t2] = my_q[t2] < p.Lq;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < NKD; ++ks) {
       bf16x8 qv = qok[t2] ? *(const bf16x8*)(Q + my_q[t2] * p.ldq + 32 * ks + 8 * g) : bf16x8{};
       df[t2][ks] = qok[t2] ? *(const bf16x8*)(dO + my_q[t2] * p.ldo + 32 * ks + 8 * g) : bf16x8{};
       float f[8];
@@ -873,27 +875,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
 
-  f32x4 dq[4][2];  // [16-row d tile][query tile]
+  f32x4 dq[NDS][2];  // [16-row d tile][query tile]
 #pragma unroll
-  for (int ds = 0; ds < 4; ++ds) dq[ds][0] = dq[ds][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ds = 0; ds < NDS; ++ds) dq[ds][0] = dq[ds][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const GldsOff go_k = glds_offsets<SW_DUAL>(p.ldk, w, lane), go_v = glds_offsets<SW_ROW>(p.ldv, w, lane);
   auto issue = [&](char* buf, long c0) {
 #pragma unroll
-    for (int sk = 0; sk < QT; ++sk) {
-      const long cc = c0 + 64 * sk;
-      char* bk = buf + sk * SUB;
-      char* bv = buf + (QT + sk) * SUB;
-      if (cc + TL <= p.Lkv) {
-        tile_glds_fast(bk, K + cc * p.ldk, go_k, w);
-        tile_glds_fast(bv, V + cc * p.ldv, go_v, w);
-      } else {
-        tile_glds<SW_DUAL>(bk, K, p.ldk, cc, p.Lkv, w, lane);
-        tile_glds<SW_ROW>(bv, V, p.ldv, cc, p.Lkv, w, lane);
+    for (int sk = 0; sk < QT; ++sk)
+#pragma unroll
+      for (int sb = 0; sb < NSUB; ++sb) {
+        const long cc = c0 + 64 * sk;
+        char* bk = buf + (sk * NSUB + sb) * SUB;
+        char* bv = buf + ((QT + sk) * NSUB + sb) * SUB;
+        if (cc + TL <= p.Lkv) {
+          tile_glds_fast(bk, K + cc * p.ldk + 64 * sb, go_k, w);
+          tile_glds_fast(bv, V + cc * p.ldv + 64 * sb, go_v, w);
+        } else {
+          tile_glds<SW_DUAL>(bk, K + 64 * sb, p.ldk, cc, p.Lkv, w, lane);
+          tile_glds<SW_ROW>(bv, V + 64 * sb, p.ldv, cc, p.Lkv, w, lane);
+        }
       }
-    }
   };
-  constexpr int OPS = 4 * QT;
+  constexpr int OPS = 4 * QT * NSUB;
   auto wait_oldest = [&](int younger) {
     if (younger > 0)
       vmcnt<OPS>();
@@ -923,8 +927,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
       const bool masked = kind == TILE_PARTIAL;
 #pragma unroll
       for (int sk = 0; sk < QT; ++sk) {
-        const char* lk = tb + sk * SUB;
-        const char* lv = tb + (QT + sk) * SUB;
+        const char* lk = tb + sk * NSUB * SUB;
+        const char* lv = tb + (QT + sk) * NSUB * SUB;
         unsigned long long bh[2] = {0ull, 0ull};
         if (masked) {
 #pragma unroll
@@ -933,6 +937,56 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
         }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
+          if constexpr (D == 128) {
+            // one 16-key row tile at a time (its S / dP chains over the four k steps, exp2, mask,
+            // dS, half of the permuted B fragment): the 32-key form spills at two waves per SIMD
+            bf16x8 sf[2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              f32x4 st[2], dp[2];
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2) {
+                st[t2] = sinit[t2];
+                dp[t2] = pinit[t2];
+              }
+#pragma unroll
+              for (int kd = 0; kd < NKD; ++kd) {
+                const bf16x8 ak = frag_row16<SW_DUAL>(lk + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
+                const bf16x8 av = frag_row16<SW_ROW>(lv + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2) {
+                  st[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t2][kd], st[t2], 0, 0, 0);
+                  dp[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df[t2][kd], dp[t2], 0, 0, 0);
+                }
+              }
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) st[t2][r] = __builtin_amdgcn_exp2f(st[t2][r]);
+              if (masked) {
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2) {
+                  if (kb == 0 && ks == 0) apply_bits4<0>(st[t2], bh[t2], 0.f);
+                  if (kb == 0 && ks == 1) apply_bits4<16>(st[t2], bh[t2], 0.f);
+                  if (kb == 1 && ks == 0) apply_bits4<32>(st[t2], bh[t2], 0.f);
+                  if (kb == 1 && ks == 1) apply_bits4<48>(st[t2], bh[t2], 0.f);
+                }
+              }
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sf[t2][4 * ks + r] = (bf16)(dp[t2][r] * st[t2][r]);
+              __builtin_amdgcn_sched_barrier(0);  // register budget: one 16-key tile's S / dP live at a time
+            }
+#pragma unroll
+            for (int ds = 0; ds < NDS; ++ds) {
+              const bf16x8 akt = frag_tr16(lk + (ds >> 2) * SUB, 32 * kb, ds & 3, lane);
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2)
+                dq[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akt, sf[t2], dq[ds][t2], 0, 0, 0);
+            }
+            continue;
+          }
           f32x4 st[2][2], dp[2][2];  // [16-row key tile][query tile]
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
@@ -942,11 +996,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
               dp[ks][t2] = pinit[t2];
             }
 #pragma unroll
-          for (int kd = 0; kd < 2; ++kd)
+          for (int kd = 0; kd < NKD; ++kd)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-              const bf16x8 ak = frag_row16<SW_DUAL>(lk, 32 * kb + 16 * ks, kd, lane);
-              const bf16x8 av = frag_row16<SW_ROW>(lv, 32 * kb + 16 * ks, kd, lane);
+              const bf16x8 ak = frag_row16<SW_DUAL>(lk + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
+              const bf16x8 av = frag_row16<SW_ROW>(lv + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
 #pragma unroll
               for (int t2 = 0; t2 < 2; ++t2) {
                 st[ks][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t2][kd], st[ks][t2], 0, 0, 0);
@@ -981,8 +1035,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
             sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
           }
 #pragma unroll
-          for (int ds = 0; ds < 4; ++ds) {
-            const bf16x8 akt = frag_tr16(lk, 32 * kb, ds, lane);
+          for (int ds = 0; ds < NDS; ++ds) {
+            const bf16x8 akt = frag_tr16(lk + (ds >> 2) * SUB, 32 * kb, ds & 3, lane);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
               dq[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akt, sf[t2], dq[ds][t2], 0, 0, 0);
@@ -998,7 +1052,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
     if (!qok[t2]) continue;
     bf16* pq = p.dq + b * p.sdqb + my_q[t2] * p.lddq + head * D + 4 * g;
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
+    for (int ds = 0; ds < NDS; ++ds) {
       bf16x4 a4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) a4[e] = (bf16)(dq[ds][t2][e] * p.scale);
@@ -1047,16 +1101,22 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
       static const int v16 = getenv("OWLK_DQ16") ? atoi(getenv("OWLK_DQ16")) : 1;  // 16x16x32 variant (0: 32x32x16)
       if (v16) {
         if (p.m.window <= 0)
-          hipLaunchKernelGGL((attn_bwd_dq16_k<2>), grid, dim3(256), 0, s, p);
+          hipLaunchKernelGGL((attn_bwd_dq16_k<64, 2>), grid, dim3(256), 0, s, p);
         else
-          hipLaunchKernelGGL((attn_bwd_dq16_k<1>), grid, dim3(256), 0, s, p);
+          hipLaunchKernelGGL((attn_bwd_dq16_k<64, 1>), grid, dim3(256), 0, s, p);
       } else if (p.m.window <= 0) {
         hipLaunchKernelGGL((attn_bwd_dq_k<D, 2>), grid, dim3(256), 0, s, p);
       } else {
         hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
       }
     } else {
-      hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
+      // D 128: the 16x16x32 form (32 queries per wave, two waves per SIMD) by default;
+      // OWLK_DQ16_128 = 0 the 32x32x16 attn_bwd_dq_k
+      static const int v16 = getenv("OWLK_DQ16_128") ? atoi(getenv("OWLK_DQ16_128")) : 1;
+      if (v16)
+        hipLaunchKernelGGL((attn_bwd_dq16_k<128, 1>), grid, dim3(256), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_k<D, 1>), grid, dim3(256), 0, s, p);
     }
     if (int e = owlk::check_launch("attn_bwd_dq")) return e;
   }
