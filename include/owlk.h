@@ -56,6 +56,19 @@ int owlk_gemm(long M, long N, long K, long batch,
               const void* gate, long ldgate, long sGate, long tpf,
               const void* resid, long ldres, long sRes,
               float* colsum, void* ws, long ws_bytes, void* stream);
+/* owlk_gemm (batch 1, no colsum) with frame-strided operand rows: with x_fs > 0, row r of that operand
+ *   lives at (r / OWLK_FRAME_ROWS) * x_fs + (r % OWLK_FRAME_ROWS) * ldx elements (the rows of A / B are
+ *   its m / n rows, or its k rows when transposed; C's are m).  The video rows of the MMDiT joint
+ *   sequence -- frame f = [64 video | 1 audio] tokens, mmattn.py:54-60 -- are read and written in
+ *   place (x_fs = 65 * ldx) with no interleave / split copies.  256^2-tile shapes only (M, N multiples
+ *   of 256 where tiled, K % 64 == 0; split-K weight gradients need the workspace); C frame-strided only
+ *   for a bf16 STORE; otherwise returns 1. */
+#define OWLK_FRAME_ROWS 64
+int owlk_gemm_frames(long M, long N, long K, const void* A, long lda, long a_fs, int a_trans,
+                     const void* B, long ldb, long b_fs, int b_trans, void* C, long ldc, long c_fs,
+                     int c_f32, int epi, float alpha, float beta, const float* bias, void* aux, long ldaux,
+                     const void* gate, long ldgate, long tpf, const void* resid, long ldres, void* ws,
+                     long ws_bytes, void* stream);
 /* bytes of split-K workspace owlk_gemm uses for these arguments (0: no split) */
 long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta);
@@ -181,6 +194,10 @@ int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpre
 long owlk_colsum_ws_bytes(long R, long N);
 int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* ws, long ws_bytes,
                 void* stream);
+/* owlk_colsum over frame-strided rows (row r at (r / OWLK_FRAME_ROWS) * fs + (r % OWLK_FRAME_ROWS) * ld;
+ * fs = 0: plain): the MMDiT video qkv bias gradient summed in place over the joint rows */
+int owlk_colsum_frames(const void* x, int x_f32, long R, long N, long ld, long fs, float* out, void* ws,
+                       long ws_bytes, void* stream);
 
 /* ---- Newton-Schulz (muon.py:11-38) helpers: X /= (||X||_F + eps) per batch item, bf16.
  * Norms are reduced without atomics: sum-of-squares passes write OWLK_NORM_PARTS partial sums per

@@ -497,21 +497,23 @@ __global__ __launch_bounds__(256) void mse_k(const bf16* __restrict__ pred, cons
 // out[n] (+)= sum_r x[r, n]; x bf16 or fp32; grid.y splits the rows.  With a workspace each split
 // stores its partial row (part[split][n]) and colsum_reduce_k adds them onto out in split order
 // (bitwise reproducible); without one, fp32 atomics combine the splits.
+// fs > 0: frame-strided rows, row r at (r / 64) * fs + (r % 64) * ld (owlk_colsum_frames)
 template <typename T, int U>
 __global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, long R, long N, long ld, long rows_per,
-                                                float* __restrict__ out, float* __restrict__ part) {
+                                                float* __restrict__ out, float* __restrict__ part, long fs) {
   const long col = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
   if (col >= N) return;
   const long r0 = (long)blockIdx.y * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto add_row = [&](long r) {
+    const long ro = fs ? (r >> 6) * fs + (r & 63) * ld : r * ld;
     if constexpr (sizeof(T) == 2) {
       float v[8];
-      unpack8(__builtin_nontemporal_load((const bf16x8*)(x + r * ld + col)), v);
+      unpack8(__builtin_nontemporal_load((const bf16x8*)(x + ro + col)), v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += v[e];
     } else {
-      const f32x4 a = *(const f32x4*)(x + r * ld + col), b = *(const f32x4*)(x + r * ld + col + 4);
+      const f32x4 a = *(const f32x4*)(x + ro + col), b = *(const f32x4*)(x + ro + col + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         acc[e] += a[e];
@@ -783,9 +785,18 @@ extern "C" long owlk_colsum_ws_bytes(long R, long N) {
   return colsum_splits(R, N, nullptr) * N * (long)sizeof(float);
 }
 
+extern "C" int owlk_colsum_frames(const void* x, int x_f32, long R, long N, long ld, long fs, float* out, void* ws,
+                                  long ws_bytes, void* stream);
+
 extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, float* out, void* ws, long ws_bytes,
                            void* stream) {
+  return owlk_colsum_frames(x, x_f32, R, N, ld, 0, out, ws, ws_bytes, stream);
+}
+
+extern "C" int owlk_colsum_frames(const void* x, int x_f32, long R, long N, long ld, long fs, float* out, void* ws,
+                                  long ws_bytes, void* stream) {
   OWLK_REQUIRE(N % 8 == 0 && ld % 8 == 0, "colsum: N, ld must be multiples of 8");
+  OWLK_REQUIRE(fs == 0 || (fs > 0 && fs % 8 == 0 && R % 64 == 0), "colsum: frame-strided rows need whole 64-row frames");
   OWLK_REQUIRE(((uintptr_t)out & 15) == 0, "colsum: out must be 16-byte aligned");
   long rows_per;
   const long splits = colsum_splits(R, N, &rows_per);
@@ -795,9 +806,9 @@ extern "C" int owlk_colsum(const void* x, int x_f32, long R, long N, long ld, fl
   dim3 g((unsigned)cols_blocks, (unsigned)splits);
   hipStream_t s = (hipStream_t)stream;
   if (x_f32)
-    hipLaunchKernelGGL((colsum_k<float, 4>), g, dim3(256), 0, s, (const float*)x, R, N, ld, rows_per, out, part);
+    hipLaunchKernelGGL((colsum_k<float, 4>), g, dim3(256), 0, s, (const float*)x, R, N, ld, rows_per, out, part, fs);
   else
-    hipLaunchKernelGGL((colsum_k<bf16, 8>), g, dim3(256), 0, s, (const bf16*)x, R, N, ld, rows_per, out, part);
+    hipLaunchKernelGGL((colsum_k<bf16, 8>), g, dim3(256), 0, s, (const bf16*)x, R, N, ld, rows_per, out, part, fs);
   if (part) return owlk::colsum_reduce(part, (int)splits, N, out, s);
   return owlk::check_launch("colsum");
 }

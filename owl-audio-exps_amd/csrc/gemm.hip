@@ -49,7 +49,19 @@ struct GemmP {
   float* colsum;      // ... and the launched kernel fuses it (set by the dispatch, else a separate pass)
   float* cs_part;     // fused column sums as per-(tile row, wave row) partials [tiles_m * 2][N] (deterministic)
   int group_m;        // gemm_pp_kernel tile order: groups of group_m tile rows (<= 1: row-major)
+  // frame-strided rows (gemm_pp_kernel only): row r of the operand lives at (r / 64) * fs + (r % 64) * ld
+  // -- the video rows of the MMDiT joint sequence (64 video + 1 audio token per frame, mmattn.py:54-60)
+  // read / written in place; 0 = plain rows r * ld
+  long a_fs, b_fs, c_fs;
 };
+
+constexpr int FRAME_ROWS = 64;  // rows per frame of a frame-strided operand (OWLK_FRAME_ROWS)
+
+// element offset of row r: plain (F = false) or frame-strided
+template <bool F>
+DEV long row_off(long r, long ld, long fs) {
+  return F ? (r >> 6) * fs + (r & 63) * ld : r * ld;
+}
 
 // 32-B block swizzle of an m/n-contiguous tile so the 8 k-rows one ds_read_b64_tr_b16 half-wave
 // touches land on distinct bank slots (256-B rows for ROWS >= 128, 128-B rows for ROWS == 64)
@@ -235,7 +247,7 @@ DEV void st_nt(bf16x8* dst, bf16x8 v) { __builtin_nontemporal_store(v, dst); }
 
 // epi_chunk with the bias (already bf16-rounded, bb) and the aux / resid (x) and gate (g) inputs
 // supplied by the caller (loaded ahead of time)
-template <int EPI, bool OF32>
+template <int EPI, bool OF32, bool CF = false>
 DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], const float (&bb)[8], const bf16x8& x,
                    const bf16x8& g, float (&cs)[8]) {
   if (EPI == EPI_STORE) {
@@ -254,7 +266,7 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
       *(f32x4*)C = f32x4{v[0], v[1], v[2], v[3]};
       *(f32x4*)(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
     } else {
-      bf16* C = (bf16*)p.C + z * p.sC + gm * p.ldc + gn;
+      bf16* C = (bf16*)p.C + z * p.sC + row_off<CF>(gm, p.ldc, p.c_fs) + gn;
       if (p.beta != 0.f) {
         float o[8];
         unpack8(*(const bf16x8*)C, o);
@@ -457,8 +469,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmP p) {
 // operands, rows of k-contiguous operands may have a ragged last tile (rows clamped).
 constexpr int NT8 = 512;
 
-template <int ROWS, bool TRANS>
-DEV void glds_tile(char* lds, const bf16* base, long ld, long r0, long k0, long R, int wave, int lane) {
+template <int ROWS, bool TRANS, bool F = false>
+DEV void glds_tile(char* lds, const bf16* base, long ld, long r0, long k0, long R, int wave, int lane, long fs = 0) {
   if (!TRANS) {  // [ROWS][64] k-contiguous: 8 rows x 128 B per wave-instruction
 #pragma unroll
     for (int i = 0; i < ROWS / 64; ++i) {
@@ -467,7 +479,8 @@ DEV void glds_tile(char* lds, const bf16* base, long ld, long r0, long k0, long 
       const int ch = (lane & 7) ^ ((row >> 1) & 7);
       long gr = r0 + row;
       gr = gr < R ? gr : R - 1;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(base + gr * ld + k0 + ch * 8),
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(base + row_off<F>(gr, ld, fs) +
+                                                                                         k0 + ch * 8),
                                        (void __attribute__((address_space(3)))*)(lds + rbase * 128), 16, 0, 0);
     }
   } else {  // [64][ROWS] m/n-contiguous: 1 KiB = 1024 / (2 ROWS) k-rows per wave-instruction
@@ -480,7 +493,7 @@ DEV void glds_tile(char* lds, const bf16* base, long ld, long r0, long k0, long 
       const int pch = lane % CPR;
       const int lch = ((((pch >> 1) ^ swz_t<ROWS>(k))) << 1) | (pch & 1);
       __builtin_amdgcn_global_load_lds(
-          (const void __attribute__((address_space(1)))*)(base + (k0 + k) * ld + r0 + lch * 8),
+          (const void __attribute__((address_space(1)))*)(base + row_off<F>(k0 + k, ld, fs) + r0 + lch * 8),
           (void __attribute__((address_space(3)))*)(lds + kb * ROWS * 2), 16, 0, 0);
     }
   }
@@ -617,8 +630,10 @@ __global__ __launch_bounds__(NT8, 1) void gemm256_kernel(GemmP p) {
 // WAR: a half-tile is re-staged only after the barrier that follows the last wave's lgkmcnt on
 // its previous contents (B last read in phase 1, A in phase 2, group 1 one barrier later).
 // RAW: every wave's vmcnt for tile t+1 precedes (in barrier order) the first read of it.
-template <bool AT, bool BT, int EPI, bool OF32>
+// FS: frame-strided rows (GemmP::a_fs / b_fs / c_fs) of A (bit 0), B (bit 1), C (bit 2; bf16 STORE)
+template <bool AT, bool BT, int EPI, bool OF32, int FS = 0>
 __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
+  constexpr bool FA = FS & 1, FB = (FS & 2) != 0, FC = (FS & 4) != 0;
   constexpr int HALF = 128 * BK * 2, STAGE = 4 * HALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -658,13 +673,13 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
 
   auto issueA = [&](int t) {
     char* st = smem + (t & 1) * STAGE;
-    glds_tile<128, AT>(st, A, p.lda, m0, kbeg + (long)t * BK, p.M, wave, lane);
-    glds_tile<128, AT>(st + HALF, A, p.lda, m0 + 128, kbeg + (long)t * BK, p.M, wave, lane);
+    glds_tile<128, AT, FA>(st, A, p.lda, m0, kbeg + (long)t * BK, p.M, wave, lane, p.a_fs);
+    glds_tile<128, AT, FA>(st + HALF, A, p.lda, m0 + 128, kbeg + (long)t * BK, p.M, wave, lane, p.a_fs);
   };
   auto issueB = [&](int t) {
     char* st = smem + (t & 1) * STAGE + 2 * HALF;
-    glds_tile<128, BT>(st, B, p.ldb, n0, kbeg + (long)t * BK, p.N, wave, lane);
-    glds_tile<128, BT>(st + HALF, B, p.ldb, n0 + 128, kbeg + (long)t * BK, p.N, wave, lane);
+    glds_tile<128, BT, FB>(st, B, p.ldb, n0, kbeg + (long)t * BK, p.N, wave, lane, p.b_fs);
+    glds_tile<128, BT, FB>(st + HALF, B, p.ldb, n0 + 128, kbeg + (long)t * BK, p.N, wave, lane, p.b_fs);
   };
   const int bcol = (wc & 1) * 64;  // first column of this wave inside its B half
   auto readA = [&](bf16x8 (&af)[4][2], const char* la, int mh) {
@@ -840,7 +855,7 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
           v[e] = lo[e];
           v[e + 4] = hi[e];
         }
-        if (gm < p.M) epi_apply<EPI, OF32>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
+        if (gm < p.M) epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -917,6 +932,45 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
   // at K >= 4608 and for split-K weight gradients row-major order measured equal or better
   static const int group_m = getenv("OWLK_GEMM_GROUP") ? atoi(getenv("OWLK_GEMM_GROUP")) : -1;
   p.group_m = group_m >= 0 ? group_m : (splits == 1 && p.kchunk <= 2048 ? 4 : 0);
+  const int fs = (p.a_fs ? 1 : 0) | (p.b_fs ? 2 : 0) | (p.c_fs ? 4 : 0);
+  if (fs) {
+    // frame-strided rows: only the combinations the MMDiT block uses are built
+    bool ok = false;
+    if constexpr (!AT && !BT && EPI == EPI_STORE && !OF32) {  // video qkv projection into the joint rows
+      if (fs == 4) {
+        hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32, 4>), grid, dim3(NT8), 0, s, p);
+        ok = true;
+      }
+    }
+    if constexpr (!AT && !BT && EPI == EPI_GATE_RESID) {  // out-projection reading the joint attention output
+      if (fs == 1) {
+        hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32, 1>), grid, dim3(NT8), 0, s, p);
+        ok = true;
+      }
+    }
+    if constexpr (!AT && BT && EPI == EPI_STORE && !OF32) {  // dX into the joint dO / from the joint dqkv
+      if (fs == 4) {
+        hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32, 4>), grid, dim3(NT8), 0, s, p);
+        ok = true;
+      }
+      if (fs == 1) {
+        hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32, 1>), grid, dim3(NT8), 0, s, p);
+        ok = true;
+      }
+    }
+    if constexpr (AT && BT && EPI == EPI_STORE && OF32) {  // weight gradients over joint rows
+      if (fs == 1) {
+        hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32, 1>), grid, dim3(NT8), 0, s, p);
+        ok = true;
+      }
+      if (fs == 2) {
+        hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32, 2>), grid, dim3(NT8), 0, s, p);
+        ok = true;
+      }
+    }
+    OWLK_REQUIRE(ok && pp, "gemm: frame-strided rows (mask %d) not built for this operand layout / epilogue", fs);
+    return owlk::check_launch("gemm256");
+  }
   if (pp)
     hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   else
@@ -1361,6 +1415,12 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32
   // atomics onto C, cleared first when beta = 0
   static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
+  const bool frames = p.a_fs || p.b_fs || p.c_fs;
+  OWLK_REQUIRE(!frames || (fits256(M, N, K, a_trans, b_trans, c_f32, beta) && batch == 1 &&
+                           (pl.kind == SPLIT_256 || pl.kind == SPLIT_NONE) &&
+                           (pl.kind != SPLIT_256 || (have_ws && !atomic_splitk)) && pl.kchunk % FRAME_ROWS == 0),
+               "gemm: frame-strided rows need the 256^2 kernel (M=%ld N=%ld K=%ld)", M, N, K);
+  if (frames && pl.kind == SPLIT_NONE) return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
   if (fits256(M, N, K, a_trans, b_trans, c_f32, beta)) {
     const long nsp = pl.kind == SPLIT_256 ? pl.splits : 1;
     if (nsp > 1) {
@@ -1438,6 +1498,25 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   if (colsum && !p.colsum)  // not fused by this kernel: a separate (workspace: deterministic) pass
     return owlk_colsum(C, 0, M, N, ldc, colsum, ws, ws_bytes, stream);
   return 0;
+}
+
+extern "C" int owlk_gemm_frames(long M, long N, long K, const void* A, long lda, long a_fs, int a_trans,
+                                const void* B, long ldb, long b_fs, int b_trans, void* C, long ldc, long c_fs,
+                                int c_f32, int epi, float alpha, float beta, const float* bias, void* aux, long ldaux,
+                                const void* gate, long ldgate, long tpf, const void* resid, long ldres, void* ws,
+                                long ws_bytes, void* stream) {
+  OWLK_REQUIRE(a_fs >= 0 && b_fs >= 0 && c_fs >= 0 && a_fs % 8 == 0 && b_fs % 8 == 0 && c_fs % 8 == 0,
+               "gemm_frames: frame strides must be non-negative multiples of 8");
+  OWLK_REQUIRE(!c_fs || (!c_f32 && epi == EPI_STORE), "gemm_frames: frame-strided C only for a bf16 STORE");
+  OWLK_REQUIRE((!a_fs || (a_trans ? K : M) % FRAME_ROWS == 0) && (!b_fs || (b_trans ? K : N) % FRAME_ROWS == 0) &&
+                   (!c_fs || M % FRAME_ROWS == 0),
+               "gemm_frames: frame-strided dims must be whole frames of %d rows", FRAME_ROWS);
+  GemmP p{};
+  p.a_fs = a_fs;
+  p.b_fs = b_fs;
+  p.c_fs = c_fs;
+  return gemm_dispatch(p, M, N, K, 1, A, lda, 0, a_trans, B, ldb, 0, b_trans, C, ldc, 0, c_f32, epi, alpha, beta, bias,
+                       aux, ldaux, 0, gate, ldgate, 0, tpf, resid, ldres, 0, ws, ws_bytes, stream);
 }
 
 extern "C" long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32,

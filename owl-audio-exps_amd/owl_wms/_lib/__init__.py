@@ -17,6 +17,7 @@ L, I, F, P = ctypes.c_long, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 _SIGS = {
     "owlk_gemm": [L, L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, L, P, L, L, L, P, L, L, P, P, L,
                   P],
+    "owlk_gemm_frames": [L, L, L, P, L, L, I, P, L, L, I, P, L, L, I, I, F, F, P, P, L, P, L, L, P, L, P, L, P],
     "owlk_gemm_splitk_bytes": [L, L, L, L, I, I, I, I, F],
     "owlk_gemm_ws_bytes": [L, L, L, L, I, I, I, I, F, I],
     "owlk_gemm_ws_counter_bytes": [L, L, L, L, I, I, I, I, F],
@@ -46,6 +47,7 @@ _SIGS = {
     "owlk_mse": [P, P, L, F, P, P, I, P],
     "owlk_colsum_ws_bytes": [L, L],
     "owlk_colsum": [P, I, L, L, L, P, P, L, P],
+    "owlk_colsum_frames": [P, I, L, L, L, L, P, P, L, P],
     "owlk_ns_normalize": [P, I, L, L, L, I, P, P, P],
     "owlk_ns_scale": [P, I, L, L, L, I, P, P, P],
     "owlk_ns_iterate_ws_bytes": [L, L, L],

@@ -23,13 +23,73 @@ def _rowmajor(t, name):
     return t
 
 
+FRAME_ROWS = 64  # OWLK_FRAME_ROWS: rows per frame of a frame-strided operand
+
+
+def frame_rows(joint, n0, n1, col0, cols):
+    """The video rows of an MMDiT joint-sequence buffer (frame f = [n0 video | n1 audio] rows,
+    mmattn.py:54-60) as a [F, n0, cols] view: row r of the video operand is joint row
+    (r // n0) (n0 + n1) + r % n0.  libowlk's GEMM / column-sum entries read and write such frame-strided
+    rows in place (owlk_gemm_frames), so no interleave / split copy of the joint buffer is made."""
+    assert n0 == FRAME_ROWS and joint.dim() == 2 and joint.stride(1) == 1
+    F_ = joint.shape[0] // (n0 + n1)
+    return joint.view(F_, n0 + n1, joint.shape[1])[:, :n0, col0:col0 + cols]
+
+
+def _operand(t, name):
+    """2-D row-major view -> (rows, cols, ld, 0); 3-D frame_rows view [F, 64, cols] -> (F*64, cols,
+    row stride, frame stride)."""
+    if t.dim() == 3:
+        assert t.shape[1] == FRAME_ROWS and t.stride(2) == 1 and t.dtype == BF16, f"{name}: frame rows view"
+        return t.shape[0] * FRAME_ROWS, t.shape[2], t.stride(1), t.stride(0)
+    _rowmajor(t, name)
+    return t.shape[0], t.shape[1], t.stride(0), 0
+
+
+def _gemm_frames(A, B, out, a_trans, b_trans, out_f32, epi, alpha, beta, bias, aux, gate, tpf, resid):
+    """gemm() with frame-strided operand rows (3-D frame_rows views): owlk_gemm_frames."""
+    ra, ca, lda, afs = _operand(A, "A")
+    rb, cb, ldb, bfs = _operand(B, "B")
+    M, K = (ca, ra) if a_trans else (ra, ca)
+    N, Kb = (cb, rb) if b_trans else (rb, cb)
+    assert K == Kb, f"gemm: K mismatch {K} vs {Kb}"
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=F32 if out_f32 else BF16)
+    if out.dim() == 3:
+        rc, cc, ldc, cfs = _operand(out, "out")
+    else:
+        assert out.dim() == 2 and out.stride(1) == 1
+        rc, cc, ldc, cfs = out.shape[0], out.shape[1], out.stride(0), 0
+    assert (rc, cc) == (M, N) and out.dtype == (F32 if out_f32 else BF16)
+    if bias is not None:
+        assert bias.dtype == F32 and bias.numel() == N and bias.is_contiguous()
+    for t, nm in ((aux, "aux"), (resid, "resid")):
+        if t is not None:
+            assert t.shape == (M, N) and t.stride(1) == 1 and t.dtype == BF16, nm
+    if gate is not None:
+        assert gate.dim() == 2 and gate.shape[1] == N and gate.stride(1) == 1 and gate.shape[0] * tpf >= M
+    ws_bytes = lib().owlk_gemm_ws_bytes(M, N, K, 1, int(a_trans), int(b_trans), int(out_f32), epi, float(beta), 0)
+    ws = torch.empty(ws_bytes, device=out.device, dtype=torch.uint8) if ws_bytes > 0 else None
+    call("owlk_gemm_frames", M, N, K, ptr(A), lda, afs, int(a_trans), ptr(B), ldb, bfs, int(b_trans),
+         ptr(out), ldc, cfs, int(out_f32), epi, float(alpha), float(beta), ptr(bias),
+         ptr(aux), aux.stride(0) if aux is not None else 0, ptr(gate), gate.stride(0) if gate is not None else 0,
+         int(tpf), ptr(resid), resid.stride(0) if resid is not None else 0, ptr(ws), ws_bytes, stream(),
+         key=f"gemm<256f,{int(a_trans)}{int(b_trans)},epi{epi},{'f32' if out_f32 else 'bf16'}>[{M}x{N}x{K}]",
+         flops=lambda: 2.0 * M * N * K)
+    return out
+
+
 def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI_STORE, alpha=1.0, beta=0.0,
          bias=None, aux=None, gate=None, tpf=1, resid=None, colsum=None):
     """C[m, n] = epi(sum_k A(m, k) B(n, k)) for 2-D views.
 
     A: [M, K] (a_trans False) or [K, M] (a_trans True); B: [N, K] or [K, N] (b_trans True).
+    A, B or out may instead be 3-D frame_rows views (frame-strided rows, the MMDiT joint layout).
     colsum: optional fp32 [N], += column sums of the stored bf16 C (fused into the DSILU epilogue).
     """
+    if A.dim() == 3 or B.dim() == 3 or (out is not None and out.dim() == 3):
+        assert colsum is None
+        return _gemm_frames(A, B, out, a_trans, b_trans, out_f32, epi, alpha, beta, bias, aux, gate, tpf, resid)
     _rowmajor(A, "A")
     _rowmajor(B, "B")
     M, K = (A.shape[1], A.shape[0]) if a_trans else (A.shape[0], A.shape[1])
@@ -100,8 +160,9 @@ def _decode_ws(device, nbytes):
 
 
 def gemm_wgrad(dy, x):
-    """fp32 weight gradient dW[n, k] = sum_m dy[m, n] x[m, k] (split-K over the token dimension)."""
-    out = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=F32)
+    """fp32 weight gradient dW[n, k] = sum_m dy[m, n] x[m, k] (split-K over the token dimension);
+    dy / x may be frame_rows views."""
+    out = torch.empty(dy.shape[-1], x.shape[-1], device=dy.device, dtype=F32)
     return gemm(dy, x, a_trans=True, b_trans=True, out=out, out_f32=True, beta=0.0)
 
 
@@ -424,14 +485,17 @@ def mse(pred, tgt, want_grad=True, grad_scale=1.0):
 
 
 def colsum(x, out=None):
-    """fp32 column sums of a 2-D row-major view, added onto out (deterministic: row-split partials
-    in a workspace, summed in order)."""
-    R, N = x.shape
+    """fp32 column sums of a 2-D row-major view (or a 3-D frame_rows view), added onto out
+    (deterministic: row-split partials in a workspace, summed in order)."""
+    if x.dim() == 3:
+        R, N, ld, fs = _operand(x, "x")
+    else:
+        (R, N), ld, fs = x.shape, x.stride(0), 0
     if out is None:
         out = torch.zeros(N, device=x.device, dtype=F32)
     nb = lib().owlk_colsum_ws_bytes(R, N)
     ws = torch.empty(nb, device=x.device, dtype=torch.uint8)
-    call("owlk_colsum", ptr(x), int(x.dtype == F32), R, N, x.stride(0), ptr(out), ptr(ws), nb, stream(),
+    call("owlk_colsum_frames", ptr(x), int(x.dtype == F32), R, N, ld, fs, ptr(out), ptr(ws), nb, stream(),
          key="owlk_colsum")
     return out
 

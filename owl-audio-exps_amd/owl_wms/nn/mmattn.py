@@ -39,6 +39,64 @@ class MMGeometry:
         self.H, self.D, self.n0, self.n1, self.mask, self.cos, self.sin = n_heads, head_dim, n0, n1, mask, cos, sin
 
 
+def _joint_views(j, n0, n1, cols):
+    """The per-modality rows of a joint-sequence buffer j [F (n0 + n1), cols] as operands that
+    libowlk reads / writes in place: the video rows as a frame-strided [F, n0, cols] view
+    (kernels.frame_rows), the audio row of every frame as a plain strided [F, cols] view."""
+    F_ = j.shape[0] // (n0 + n1)
+    return K.frame_rows(j, n0, n1, 0, cols), j.view(F_, n0 + n1, cols)[:, n0, :]
+
+
+def _in_place_ok(d, n0, n1):
+    """The joint layout is used in place (no frame_mux copies) where the video GEMMs tile by 256
+    (owlk_gemm_frames): mmdit_v2 (d 1536, 8x8 latents + 1 audio token per frame)."""
+    return n0 == K.FRAME_ROWS and n1 == 1 and d % 256 == 0
+
+
+_AUDIO_STREAMS = {}
+
+
+class _AudioLane:
+    """The audio modality's per-block work (adaln, its 1,000-row GEMMs, gate / adaln backward) on a
+    side HIP stream beside the video's: at mmdit_v2 the audio rows are 1/64 of the video's, so their
+    GEMMs fill few CUs and run at a fifth of the video GEMMs' rate (3 % of the micro-step serially).
+    fork(): the side stream waits for everything enqueued so far; join(): the caller's stream waits
+    for the side stream.  Tensors the side stream allocates are marked for the caller's stream
+    (record_stream), so the caching allocator never hands their blocks to later side-stream work while
+    the caller's stream may still read them.  Serial (no side stream) for the frame_mux layout, while a
+    profile window is open or a graph is being captured, or with OWLK_MMDIT_AUDIO_STREAM=0."""
+
+    def __init__(self, device, enable):
+        import os
+        from .. import _lib
+        self.main = torch.cuda.current_stream(device)
+        self.side = None
+        if enable and os.environ.get("OWLK_MMDIT_AUDIO_STREAM", "1") != "0" and not _lib.profiling() and \
+                not torch.cuda.is_current_stream_capturing():
+            self.side = _AUDIO_STREAMS.get(device)
+            if self.side is None:
+                self.side = _AUDIO_STREAMS[device] = torch.cuda.Stream(device=device)
+
+    def fork(self):
+        if self.side is not None:
+            self.side.wait_stream(self.main)
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
+
+    def on(self, s):
+        """context for modality s's work: the side stream for audio (s = 1)"""
+        import contextlib
+        return torch.cuda.stream(self.side) if (s == 1 and self.side is not None) else contextlib.nullcontext()
+
+    def mark(self, ts):
+        if self.side is not None:
+            for t in ts:
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(self.main)
+
+
 class MMDiTBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, x1, c0, c1, geo, *w):
@@ -50,35 +108,48 @@ class MMDiTBlockFn(torch.autograd.Function):
         ms = (c0.reshape(nf, 6 * d), c1.reshape(nf, 6 * d))
         ns = (n0, n1)
         W = [w[0:2], w[2:4]], [w[4:6], w[6:8]], [w[8:12], w[12:16]]  # qkv, out, mlp (fc1 w/b, fc2 w/b)
-        h1, r1, qkv = [], [], []
-        for s in range(2):
-            h, r = K.adaln_fwd(xs[s], ms[s][:, :d], ms[s][:, d:2 * d], ns[s])
-            h1.append(h)
-            r1.append(r)
-            qkv.append(K.gemm(h, bf16_weight(W[0][s][0]), bias=W[0][s][1]))
-        qkvj = K.frame_interleave(qkv[0], qkv[1], n0, n1)
+        inplace = _in_place_ok(d, n0, n1)
+        lane = _AudioLane(x0.device, inplace)
+        h1, r1, qkv = [None, None], [None, None], [None, None]
+        if inplace:  # each modality's qkv projection writes its rows of the joint frames directly
+            qkvj = torch.empty(B * T, 3 * d, device=x0.device, dtype=BF16)
+            qkv_dst = _joint_views(qkvj, n0, n1, 3 * d)
+        wq = [bf16_weight(W[0][s][0]) for s in range(2)]
+        lane.fork()
+        for s in (1, 0):  # audio first: its launches go to the side stream, then the video's run beside
+            with lane.on(s):
+                h1[s], r1[s] = K.adaln_fwd(xs[s], ms[s][:, :d], ms[s][:, d:2 * d], ns[s])
+                qkv[s] = K.gemm(h1[s], wq[s], bias=W[0][s][1], out=qkv_dst[s] if inplace else None)
+        lane.mark(h1[1:] + r1[1:])
+        lane.join()
+        if not inplace:
+            qkvj = K.frame_interleave(qkv[0], qkv[1], n0, n1)
         del qkv
         qkr, rq = K.qk_rope_fwd(qkvj, H, D, geo.cos, geo.sin, 0, T)
         q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
         o, lse = K.attn_fwd(q3, k3, qkvj.view(B, T, 3 * d)[:, :, 2 * d:], H, D, geo.mask,
                             score_bound=K.qk_norm_bound(D))
-        os_ = K.frame_split(o.view(B * T, d), n0, n1)
-        saved, outs = [], []
-        for s in range(2):
-            g1, g2 = ms[s][:, 2 * d:3 * d], ms[s][:, 5 * d:]
-            M = xs[s].shape[0]
-            y1 = torch.empty(M, d, device=x0.device, dtype=BF16)
-            x1s = K.gemm(os_[s], bf16_weight(W[1][s][0]), bias=W[1][s][1], epi=K.EPI_GATE_RESID, aux=y1, gate=g1,
-                         tpf=ns[s], resid=xs[s])
-            h2, r2 = K.adaln_fwd(x1s, ms[s][:, 3 * d:4 * d], ms[s][:, 4 * d:5 * d], ns[s])
-            fc1w, fc1b, fc2w, fc2b = W[2][s]
-            a_pre = torch.empty(M, fc1w.shape[0], device=x0.device, dtype=BF16)
-            a = K.gemm(h2, bf16_weight(fc1w), bias=fc1b, epi=K.EPI_SILU, aux=a_pre)
-            y2 = torch.empty(M, d, device=x0.device, dtype=BF16)
-            outs.append(K.gemm(a, bf16_weight(fc2w), bias=fc2b, epi=K.EPI_GATE_RESID, aux=y2, gate=g2, tpf=ns[s],
-                               resid=x1s))
-            saved += [xs[s], ms[s], h1[s], r1[s], y1, x1s, h2, r2, a_pre, a, y2]
-        ctx.save_for_backward(qkvj, qkr, rq, o, lse, *saved, *w)
+        os_ = _joint_views(o.view(B * T, d), n0, n1, d) if inplace else K.frame_split(o.view(B * T, d), n0, n1)
+        saved, outs = [None, None], [None, None]
+        wts = [[bf16_weight(W[1][s][0]), bf16_weight(W[2][s][0]), bf16_weight(W[2][s][2])] for s in range(2)]
+        lane.fork()
+        for s in (1, 0):
+            with lane.on(s):
+                g1, g2 = ms[s][:, 2 * d:3 * d], ms[s][:, 5 * d:]
+                M = xs[s].shape[0]
+                y1 = torch.empty(M, d, device=x0.device, dtype=BF16)
+                x1s = K.gemm(os_[s], wts[s][0], bias=W[1][s][1], epi=K.EPI_GATE_RESID, aux=y1, gate=g1, tpf=ns[s],
+                             resid=xs[s])
+                h2, r2 = K.adaln_fwd(x1s, ms[s][:, 3 * d:4 * d], ms[s][:, 4 * d:5 * d], ns[s])
+                a_pre = torch.empty(M, W[2][s][0].shape[0], device=x0.device, dtype=BF16)
+                a = K.gemm(h2, wts[s][1], bias=W[2][s][1], epi=K.EPI_SILU, aux=a_pre)
+                y2 = torch.empty(M, d, device=x0.device, dtype=BF16)
+                outs[s] = K.gemm(a, wts[s][2], bias=W[2][s][3], epi=K.EPI_GATE_RESID, aux=y2, gate=g2, tpf=ns[s],
+                                 resid=x1s)
+                saved[s] = [xs[s], ms[s], h1[s], r1[s], y1, x1s, h2, r2, a_pre, a, y2]
+        lane.mark(saved[1][4:] + [outs[1]])
+        lane.join()
+        ctx.save_for_backward(qkvj, qkr, rq, o, lse, *saved[0], *saved[1], *w)
         ctx.geo, ctx.dims = geo, (B, T0, x1.shape[1], d, T, nf)
         return outs[0].view(B, T0, d), outs[1].view(B, x1.shape[1], d)
 
@@ -93,30 +164,42 @@ class MMDiTBlockFn(torch.autograd.Function):
         ns = (n0, n1)
         dW = [None] * 16
         douts = (dout0.reshape(-1, d).to(BF16).contiguous(), dout1.reshape(-1, d).to(BF16).contiguous())
-        os_ = K.frame_split(o.view(B * T, d), n0, n1)
-        dos, dx1s, dmods = [], [], [[None] * 4, [None] * 4]
-        for s in range(2):
-            xs, ms, h1, r1, y1, x1s, h2, r2, a_pre, a, y2 = st[s]
-            fc1w, fc2w, wout = w[8 + 4 * s], w[10 + 4 * s], w[4 + 2 * s]
-            # ---- MLP
-            dy2, dg2, dbf2 = K.gate_bwd(douts[s], y2, ms[:, 5 * d:], ns[s])
-            dW[11 + 4 * s] = dbf2.sum(0)
-            dW[9 + 4 * s] = torch.zeros(a_pre.shape[1], device=a_pre.device, dtype=torch.float32)
-            dapre = K.gemm(dy2, bf16_weight(fc2w), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=dW[9 + 4 * s])
-            dW[10 + 4 * s] = K.gemm_wgrad(dy2, a)
-            dW[8 + 4 * s] = K.gemm_wgrad(dapre, h2)
-            dh2 = K.gemm(dapre, bf16_weight(fc1w), b_trans=True)
-            del dapre, dy2
-            dx1, dmod2 = K.adaln_bwd(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dres=douts[s])
-            # ---- attention output projection
-            dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, ms[:, 2 * d:3 * d], ns[s])
-            dW[5 + 2 * s] = dbf1.sum(0)
-            dos.append(K.gemm(dy1, bf16_weight(wout), b_trans=True))
-            dW[4 + 2 * s] = K.gemm_wgrad(dy1, os_[s])
-            dx1s.append(dx1)
-            dmods[s][1], dmods[s][2], dmods[s][3] = dg1, dmod2, dg2
+        inplace = _in_place_ok(d, n0, n1)
+        lane = _AudioLane(o.device, inplace)
+        if inplace:  # per-modality views of the joint o, and the joint dO the two dX GEMMs write into
+            os_ = _joint_views(o.view(B * T, d), n0, n1, d)
+            do = torch.empty(B * T, d, device=o.device, dtype=BF16)
+            do_dst = _joint_views(do, n0, n1, d)
+        else:
+            os_ = K.frame_split(o.view(B * T, d), n0, n1)
+        dos, dx1s, dmods = [None, None], [None, None], [[None] * 4, [None] * 4]
+        wts = [[bf16_weight(w[10 + 4 * s]), bf16_weight(w[8 + 4 * s]), bf16_weight(w[4 + 2 * s])] for s in range(2)]
+        lane.fork()
+        for s in (1, 0):
+            with lane.on(s):
+                xs, ms, h1, r1, y1, x1s, h2, r2, a_pre, a, y2 = st[s]
+                # ---- MLP
+                dy2, dg2, dbf2 = K.gate_bwd(douts[s], y2, ms[:, 5 * d:], ns[s])
+                dW[11 + 4 * s] = dbf2.sum(0)
+                dW[9 + 4 * s] = torch.zeros(a_pre.shape[1], device=a_pre.device, dtype=torch.float32)
+                dapre = K.gemm(dy2, wts[s][0], b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=dW[9 + 4 * s])
+                dW[10 + 4 * s] = K.gemm_wgrad(dy2, a)
+                dW[8 + 4 * s] = K.gemm_wgrad(dapre, h2)
+                dh2 = K.gemm(dapre, wts[s][1], b_trans=True)
+                del dapre, dy2
+                dx1, dmod2 = K.adaln_bwd(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dres=douts[s])
+                # ---- attention output projection
+                dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, ms[:, 2 * d:3 * d], ns[s])
+                dW[5 + 2 * s] = dbf1.sum(0)
+                dos[s] = K.gemm(dy1, wts[s][2], b_trans=True, out=do_dst[s] if inplace else None)
+                dW[4 + 2 * s] = K.gemm_wgrad(dy1, os_[s])
+                dx1s[s] = dx1
+                dmods[s][1], dmods[s][2], dmods[s][3] = dg1, dmod2, dg2
+        lane.mark([dW[i] for i in (6, 7, 12, 13, 14, 15)] + [dx1s[1]] + dmods[1][1:] + [dos[1]])  # audio's
+        lane.join()
         del os_
-        do = K.frame_interleave(dos[0], dos[1], n0, n1)
+        if not inplace:
+            do = K.frame_interleave(dos[0], dos[1], n0, n1)
         del dos
         dqkvj = torch.empty(B * T, 3 * d, device=o.device, dtype=BF16)
         dqkr = torch.empty(B * T, 2 * d, device=o.device, dtype=BF16)
@@ -127,19 +210,23 @@ class MMDiTBlockFn(torch.autograd.Function):
         del do
         K.qk_rope_bwd(dqkr, qkvj, rq, H, D, geo.cos, geo.sin, dqkvj, 0, T)
         del dqkr
-        dqkv = K.frame_split(dqkvj, n0, n1)
-        del dqkvj
-        dxs, dcs = [], []
-        for s in range(2):
-            xs, ms, h1, r1 = st[s][:4]
-            wq = w[2 * s]
-            dW[1 + 2 * s] = K.colsum(dqkv[s])
-            dW[2 * s] = K.gemm_wgrad(dqkv[s], h1)
-            dh1 = K.gemm(dqkv[s], bf16_weight(wq), b_trans=True)
-            dx, dmod1 = K.adaln_bwd(dh1, xs, r1, ms[:, :d], ns[s], dres=dx1s[s])
-            dxs.append(dx)
-            _, dg1, dmod2, dg2 = dmods[s]
-            dcs.append(torch.cat([dmod1, dg1, dmod2, dg2], dim=1).view(B, nf // B, 6 * d))
+        # the per-modality qkv gradients: views of the joint rows (in place) or split copies
+        dqkv = _joint_views(dqkvj, n0, n1, 3 * d) if inplace else K.frame_split(dqkvj, n0, n1)
+        dxs, dcs = [None, None], [None, None]
+        wq = [bf16_weight(w[2 * s]) for s in range(2)]
+        lane.fork()
+        for s in (1, 0):
+            with lane.on(s):
+                xs, ms, h1, r1 = st[s][:4]
+                dW[1 + 2 * s] = K.colsum(dqkv[s])
+                dW[2 * s] = K.gemm_wgrad(dqkv[s], h1)
+                dh1 = K.gemm(dqkv[s], wq[s], b_trans=True)
+                dx, dmod1 = K.adaln_bwd(dh1, xs, r1, ms[:, :d], ns[s], dres=dx1s[s])
+                dxs[s] = dx
+                _, dg1, dmod2, dg2 = dmods[s]
+                dcs[s] = torch.cat([dmod1, dg1, dmod2, dg2], dim=1).view(B, nf // B, 6 * d)
+        lane.mark([dW[3], dW[2], dxs[1], dcs[1]])
+        lane.join()
         return (dxs[0].view(B, T0, d), dxs[1].view(B, T1, d), dcs[0], dcs[1], None, *dW)
 
 

@@ -274,6 +274,38 @@ def test_mmdit_kv_cache_decode_matches_full_forward(n_ctx):
     assert rel(lv, fv[:, n_ctx:]) < 2e-2 and rel(la, fa[:, n_ctx:]) < 2e-2
 
 
+@pytest.mark.parametrize("heads", [4, 2])
+def test_mmdit_joint_rows_in_place_equals_frame_mux(heads, monkeypatch):
+    """MMDiTBlockFn with the joint 65-token frame layout read and written in place (video GEMMs on
+    frame-strided rows, owlk_gemm_frames / owlk_colsum_frames; audio rows as plain strided views)
+    == the same block through the frame_mux interleave / split copies (mmattn.py:54-60, 77-80):
+    outputs and every gradient within bf16 GEMM tolerance (d 256, head_dim 64 and 128)."""
+    from owl_wms.configs import model_config
+    from owl_wms.models.gamerft_audio import GameRFTAudio
+    from owl_wms.nn import mmattn
+    cfg = dict(MMCFG, d_model=256, n_heads=heads, n_frames=8)
+    res = []
+    for inplace in (True, False):
+        if not inplace:
+            monkeypatch.setattr(mmattn, "_in_place_ok", lambda *a: False)
+        m = det_init_(GameRFTAudio(model_config(**cfg)), base_seed=5100).cuda().train()
+        B, n = 2, 8
+        x = det_tensor((B, n, 32, 8, 8), 920).cuda().bfloat16()
+        au = det_tensor((B, n, 16), 921).cuda().bfloat16()
+        t = torch.sigmoid(det_tensor((B, n), 922)).cuda().bfloat16()
+        mouse = det_tensor((B, n, 2), 923).cuda().bfloat16()
+        btn = (det_tensor((B, n, 11), 924) > 0).cuda().bfloat16()
+        pv, pa = m.core(x, au, t, mouse, btn)
+        (pv.float().square().mean() + pa.float().square().mean()).backward()
+        res.append((pv.float(), pa.float(),
+                    {k: p.grad.float() for k, p in m.named_parameters() if p.grad is not None}))
+    (v1, a1, g1), (v2, a2, g2) = res
+    assert rel(v1, v2) < 1e-2 and rel(a1, a2) < 1e-2
+    assert g1.keys() == g2.keys() and len(g1) > 20
+    for k in g2:
+        assert rel(g1[k], g2[k]) < 2e-2, (k, rel(g1[k], g2[k]))
+
+
 class _Draws:
     """Replay torch.randn / randn_like draws (reference order) on the draw's device/dtype."""
 
