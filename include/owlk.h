@@ -86,16 +86,19 @@ long owlk_gemm_ws_counter_bytes(long M, long N, long K, long batch, int a_trans,
 int owlk_adaln_fwd(const void* x, long ldx, const void* scale, const void* shift, long ldm, long tpf,
                    long T, int d, void* y, long ldy, float* rstd, void* yact /* optional bf16(silu(y)),
                    FinalLayer attn.py:272-277 */, void* stream);
-/* backward: dx = rms_norm' (dy * (1 + scale)) (+ dres); dscale[f] = sum_t dy*xn; dshift[f] = sum_t dy */
+/* backward: dx = rms_norm' (dy * (1 + scale)) (+ dres); dscale[f] = sum_t dy*xn; dshift[f] = sum_t dy
+ *   (fp32, or bf16 with mod_bf16 = 1: straight into a bf16 modulation-gradient matrix, row stride ldg) */
 int owlk_adaln_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd,
                    const void* scale, long ldm, long tpf, long T, int d, const void* dres, long ldres,
-                   void* dx, long lddx, float* dscale, float* dshift, long ldg,
-                   const void* ypre /* optional: dy is d silu(ypre) */, void* stream);
+                   void* dx, long lddx, void* dscale, void* dshift, long ldg,
+                   const void* ypre /* optional: dy is d silu(ypre) */, int mod_bf16, void* stream);
 
 /* ---- Gate backward (modulation.py:28-43 Gate / :57-63 cond_gate; forward is GEMM epi 2):
- *   dy = bf16(dout * g[t/tpf]); dg[f] = sum_t dout*y; dbias_frames[f] = sum_t dy (optional) */
+ *   dy = bf16(dout * g[t/tpf]); dg[f] = sum_t dout*y (row stride lddg; fp32, or bf16 with dg_bf16 = 1);
+ *   dbias_frames[f] = sum_t dy (optional, fp32, row stride ldr) */
 int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const void* g, long ldg, long tpf,
-                  long T, int d, void* dy, long lddy, float* dg, float* dbias_frames, long ldr, void* stream);
+                  long T, int d, void* dy, long lddy, void* dg, long lddg, int dg_bf16, float* dbias_frames,
+                  long ldr, void* stream);
 
 /* ---- QK RMSNorm + RoPE (attn.py:83-89, rope.py:43-51): qkv rows [q(h d)|k(h d)|v(h d)] ->
  *   out rows [rope(bf16(rms(q)))|rope(bf16(rms(k)))], rotation pairs (2i, 2i+1) written to
@@ -185,9 +188,13 @@ int owlk_flow_noise(const void* x, const void* z, const float* ts_raw, int C, in
                     void* tgt, float* ts_out, void* stream);
 /* token-major [BN*P, C] -> [BN, C, P] (gamerft.py:58) */
 int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out, void* stream);
-/* MSE (gamerft.py:111): partial[block] = sum (pred - tgt)^2; dpred = bf16(gscale * (pred - tgt)) */
+/* MSE (gamerft.py:111): partial[block] = sum (pred - tgt)^2; dpred (optional) = bf16(gscale * (pred - tgt));
+ * loss (optional, fp32 scalar) = (float)(double sum of the partials in block order) / n */
 int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,
-             int nblocks, void* stream);
+             int nblocks, float* loss, void* stream);
+/* its backward: dpred = bf16((gscale * (pred - tgt)) * gout[0]) (gout NULL: 1), gscale = 2 / n for the mean */
+int owlk_mse_grad(const void* pred, const void* tgt, long n, float gscale, const float* gout, void* dpred,
+                  void* stream);
 /* out[n] += sum_r x[r, n] (bias gradients); x bf16 (x_f32 = 0) or fp32.  With ws (>=
  * owlk_colsum_ws_bytes(R, N) bytes, 16-B aligned) row splits store partial rows that one pass adds
  * in order (bitwise deterministic); without it the splits combine by fp32 atomics. */
@@ -224,6 +231,35 @@ int owlk_ns_iterate(void* x, long batch, long m, long k, int steps, float a, flo
 long owlk_newton_schulz_ws_bytes(long batch, long rows, long cols);
 int owlk_newton_schulz_bf16(const void* g, int g_f32, long batch, long rows, long cols, int steps, float a,
                             float b, float c, void* out, void* ws, long ws_bytes, void* stream);
+
+/* ---- per-frame conditioning (cond.hip; GameRFTCore.cond gamerft.py:39-48, embeddings.py:30-184,
+ *   the silu(cond) of every modulation fc modulation.py:13,32).  Each op rounds as the reference's
+ *   torch op does: to bf16 when its input is bf16 (*_f32 = 0), not at all when fp32 (*_f32 = 1);
+ *   every output is the bf16 operand autocast hands the next Linear.
+ * owlk_cond_embed: R rows ->
+ *   ts_in [R, 2 ht] = [sin e | cos e], e = (ts * tmult) * tfreq[i] (SinCosEmbed; tfreq fp32 [ht]);
+ *   mouse_in [R, 4 hm]: [:, :2 hm] = angle_proj(cos, sin of the symlog polar angle) with wang fp32 [2 hm, 2]
+ *     (bf16 operands, fp32 sum), [:, 2 hm:] = SinCos(|symlog mouse|) (mfreq fp32 [hm]); mouse row stride ldm;
+ *     ang [R, 2] bf16 = (cos, sin), kept for the angle_proj weight gradient;
+ *   btn_in [R, nbp] = 2 b - 1 (columns nb .. nbp zero).  ts / mouse / btn may each be NULL. */
+int owlk_cond_embed(const void* ts, int ts_f32, const float* tfreq, int ht, float tmult, void* ts_in, long ldt,
+                    const void* mouse, int mouse_f32, long ldm, const float* mfreq, int hm, float mmult,
+                    const float* wang, void* mouse_in, long ldmi, void* ang, const void* btn, int btn_f32, long ldb,
+                    int nb, int nbp, void* btn_in, long ldbi, long R, void* stream);
+/* cond = bf16(t + (hc[row / rows_per] ? bf16(m + b) : 0)) (m, b NULL: cond = t; hc: bool per sample,
+ * NULL: all true); s = bf16(silu(cond)); cond may be NULL (not kept).  Contiguous [R, d] bf16. */
+int owlk_cond_silu_fwd(const void* t, const void* m, const void* b, const void* hc, long rows_per, long R, int d,
+                       void* cond, void* s, void* stream);
+/* backward: ds [R, d] (fp32: all consumers of s, summed; or bf16 with ds_bf16 = 1) ->
+ * dcond = bf16(bf16(ds) silu'(cond)) (cond NULL: dcond = ds, the gradient of cond itself);
+ * dctrl = hc ? dcond : 0.  dcond / dctrl optional. */
+int owlk_cond_silu_bwd(const void* ds, int ds_bf16, const void* cond, const void* hc, long rows_per, long R, int d,
+                       void* dcond, void* dctrl, void* stream);
+/* dw[n, k] (row stride ldw, fp32) = beta * dw + sum_r dy[r, n] * x[r, k] for k < K <= 16, rows in a
+ * fixed order: the weight gradients of the embeddings' K = 2 / 11 input layers (angle_proj,
+ * button fc1), which the 8-aligned GEMM does not tile */
+int owlk_small_k_wgrad(const void* dy, long lddy, const void* x, long ldx, long R, long N, int K, float* dw,
+                       long ldw, float beta, void* stream);
 
 /* ---- fused Muon passes (optim.hip; replace muon.py:66-84's torch elementwise ops) ----
  * owlk_muon_momentum: for each of `count` fp32 matrices of n elements (host array of device

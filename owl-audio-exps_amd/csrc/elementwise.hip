@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
                                                    const bf16* __restrict__ dres, long ldres,
                                                    bf16* __restrict__ dx, long lddx,
                                                    float* __restrict__ dsc, float* __restrict__ dsh, long ldg,
-                                                   const bf16* __restrict__ ypre) {
+                                                   const bf16* __restrict__ ypre, int mod_bf16) {
   extern __shared__ float red[];  // [4][2][d]
   const long f = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -155,8 +155,13 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
       sa += red[(ww * 2 + 0) * d + j];
       sb += red[(ww * 2 + 1) * d + j];
     }
-    dsc[f * ldg + j] = sa;
-    dsh[f * ldg + j] = sb;
+    if (mod_bf16) {  // straight into the bf16 modulation-gradient matrix (fused.CondModFn)
+      ((bf16*)dsc)[f * ldg + j] = (bf16)sa;
+      ((bf16*)dsh)[f * ldg + j] = (bf16)sb;
+    } else {
+      dsc[f * ldg + j] = sa;
+      dsh[f * ldg + j] = sb;
+    }
   }
 }
 
@@ -168,7 +173,8 @@ __global__ __launch_bounds__(256) void gate_bwd_k(const bf16* __restrict__ dout,
                                                   const bf16* __restrict__ y, long ldy,
                                                   const bf16* __restrict__ g, long ldg, long tpf, int d,
                                                   bf16* __restrict__ dy, long lddy,
-                                                  float* __restrict__ dg, float* __restrict__ dbf, long ldr) {
+                                                  float* __restrict__ dg, float* __restrict__ dbf, long ldr,
+                                                  int dg_bf16, long lddg) {
   extern __shared__ float red[];
   const long f = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -218,7 +224,10 @@ __global__ __launch_bounds__(256) void gate_bwd_k(const bf16* __restrict__ dout,
       sa += red[(ww * 2 + 0) * d + j];
       sb += red[(ww * 2 + 1) * d + j];
     }
-    dg[f * ldr + j] = sa;
+    if (dg_bf16)
+      ((bf16*)dg)[f * lddg + j] = (bf16)sa;
+    else
+      dg[f * lddg + j] = sa;
     if (dbf) dbf[f * ldr + j] = sb;
   }
 }
@@ -493,6 +502,37 @@ __global__ __launch_bounds__(256) void mse_k(const bf16* __restrict__ pred, cons
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// loss = (float)(sum of the partials in double, in block order) / n: one workgroup, fixed order
+__global__ __launch_bounds__(64) void mse_finish_k(const float* __restrict__ partial, int nb, long n,
+                                                   float* __restrict__ loss) {
+  __shared__ double red[64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 64) acc += (double)partial[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < 64; ++i) s += red[i];
+    loss[0] = (float)s / (float)n;
+  }
+}
+
+// backward of F.mse_loss (fp32 math under autocast): dpred = bf16((gscale (pred - tgt)) g), g the
+// loss gradient read on the device (null: 1)
+__global__ __launch_bounds__(256) void mse_grad_k(const bf16* __restrict__ pred, const bf16* __restrict__ tgt, long n8,
+                                                  float gscale, const float* __restrict__ gout,
+                                                  bf16* __restrict__ dpred) {
+  const float go = gout ? gout[0] : 1.f;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float p[8], t[8], g[8];
+    unpack8(((const bf16x8*)pred)[i], p);
+    unpack8(((const bf16x8*)tgt)[i], t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (gscale * (p[e] - t[e])) * go;
+    ((bf16x8*)dpred)[i] = pack8(g);
+  }
+}
+
 // ------------------------------------------------------------------ column sums (bias grads)
 // out[n] (+)= sum_r x[r, n]; x bf16 or fp32; grid.y splits the rows.  With a workspace each split
 // stores its partial row (part[split][n]) and colsum_reduce_k adds them onto out in split order
@@ -613,24 +653,25 @@ extern "C" int owlk_adaln_fwd(const void* x, long ldx, const void* scale, const 
 
 extern "C" int owlk_adaln_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd,
                               const void* scale, long ldm, long tpf, long T, int d, const void* dres, long ldres,
-                              void* dx, long lddx, float* dscale, float* dshift, long ldg, const void* ypre,
-                              void* stream) {
+                              void* dx, long lddx, void* dscale, void* dshift, long ldg, const void* ypre,
+                              int mod_bf16, void* stream) {
   OWLK_REQUIRE(d % 8 == 0 && d <= 64 * 8 * MAXCPL && tpf > 0 && T % tpf == 0, "adaln_bwd: bad d=%d tpf=%ld T=%ld", d,
                tpf, T);
   OWLK_CPL_DISPATCH(d, adaln_bwd_k, dim3((unsigned)(T / tpf)), dim3(256), 8 * d * sizeof(float), (hipStream_t)stream,
                      (const bf16*)dy, lddy, (const bf16*)x, ldx, rstd, (const bf16*)scale, ldm, tpf, d,
-                     (const bf16*)dres, ldres, (bf16*)dx, lddx, dscale, dshift, ldg, (const bf16*)ypre);
+                     (const bf16*)dres, ldres, (bf16*)dx, lddx, (float*)dscale, (float*)dshift, ldg, (const bf16*)ypre,
+                     mod_bf16);
   return owlk::check_launch("adaln_bwd");
 }
 
 extern "C" int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const void* g, long ldg, long tpf,
-                             long T, int d, void* dy, long lddy, float* dg, float* dbias_frames, long ldr,
-                             void* stream) {
+                             long T, int d, void* dy, long lddy, void* dg, long lddg, int dg_bf16,
+                             float* dbias_frames, long ldr, void* stream) {
   OWLK_REQUIRE(d % 8 == 0 && d <= 64 * 8 * MAXCPL && tpf > 0 && T % tpf == 0, "gate_bwd: bad d=%d tpf=%ld T=%ld", d,
                tpf, T);
   OWLK_CPL_DISPATCH(d, gate_bwd_k, dim3((unsigned)(T / tpf)), dim3(256), 8 * d * sizeof(float), (hipStream_t)stream,
-                     (const bf16*)dout, ldo, (const bf16*)y, ldy, (const bf16*)g, ldg, tpf, d, (bf16*)dy, lddy, dg,
-                     dbias_frames, ldr);
+                     (const bf16*)dout, ldo, (const bf16*)y, ldy, (const bf16*)g, ldg, tpf, d, (bf16*)dy, lddy,
+                     (float*)dg, dbias_frames, ldr, dg_bf16, lddg);
   return owlk::check_launch("gate_bwd");
 }
 
@@ -759,11 +800,25 @@ extern "C" int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out
 }
 
 extern "C" int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,
-                        int nblocks, void* stream) {
+                        int nblocks, float* loss, void* stream) {
   OWLK_REQUIRE(n % 8 == 0 && nblocks > 0, "mse: n=%ld must be a multiple of 8", n);
   hipLaunchKernelGGL(mse_k, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const bf16*)pred, (const bf16*)tgt,
                      n / 8, gscale, (bf16*)dpred, partial);
+  if (loss) {
+    if (int rc = owlk::check_launch("mse")) return rc;
+    hipLaunchKernelGGL(mse_finish_k, dim3(1), dim3(64), 0, (hipStream_t)stream, partial, nblocks, n, loss);
+  }
   return owlk::check_launch("mse");
+}
+
+extern "C" int owlk_mse_grad(const void* pred, const void* tgt, long n, float gscale, const float* gout, void* dpred,
+                             void* stream) {
+  OWLK_REQUIRE(n % 8 == 0 && dpred, "mse_grad: n=%ld must be a multiple of 8", n);
+  const long n8 = n / 8;
+  const long nb = (n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048;
+  hipLaunchKernelGGL(mse_grad_k, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)pred,
+                     (const bf16*)tgt, n8, gscale, gout, (bf16*)dpred);
+  return owlk::check_launch("mse_grad");
 }
 
 // enough row splits to fill the chip (~2k workgroups), but >= 16 rows per workgroup: in the atomic

@@ -22,8 +22,12 @@ _SIGS = {
     "owlk_gemm_ws_bytes": [L, L, L, L, I, I, I, I, F, I],
     "owlk_gemm_ws_counter_bytes": [L, L, L, L, I, I, I, I, F],
     "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
-    "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, P],
-    "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, P, L, P],
+    "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, I, P],
+    "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, L, I, P, L, P],
+    "owlk_cond_embed": [P, I, P, I, F, P, L, P, I, L, P, I, F, P, P, L, P, P, I, L, I, I, P, L, L, P],
+    "owlk_cond_silu_fwd": [P, P, P, P, L, L, I, P, P, P],
+    "owlk_cond_silu_bwd": [P, I, P, P, L, L, I, P, P, P],
+    "owlk_small_k_wgrad": [P, L, P, L, L, L, I, P, L, F, P],
     "owlk_qk_rope_fwd": [P, L, L, I, I, P, P, L, L, L, P, L, P, P],
     "owlk_qk_rope_fwd_kv": [P, L, L, L, I, I, P, P, L, L, P, L, L, P, L, L, P, L, L, P],
     "owlk_qk_rope_fwd_kv_dev": [P, L, L, L, I, I, P, P, L, P, P, L, L, P, L, L, P, L, L, P],
@@ -44,7 +48,8 @@ _SIGS = {
                          P, P, P, P, L, P],
     "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
     "owlk_unpatchify": [P, I, I, L, P, P],
-    "owlk_mse": [P, P, L, F, P, P, I, P],
+    "owlk_mse": [P, P, L, F, P, P, I, P, P],
+    "owlk_mse_grad": [P, P, L, F, P, P, P],
     "owlk_colsum_ws_bytes": [L, L],
     "owlk_colsum": [P, I, L, L, L, P, P, L, P],
     "owlk_colsum_frames": [P, I, L, L, L, L, P, P, L, P],

@@ -205,19 +205,36 @@ def adaln_bwd(dy, x, rstd, scale, tpf, dres=None, ypre=None):
     dmod = torch.empty(F_, 2 * d, device=x.device, dtype=F32)
     call("owlk_adaln_bwd", ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(rstd), ptr(scale), scale.stride(0), tpf,
          T, d, ptr(dres), dres.stride(0) if dres is not None else 0, ptr(dx), d, ptr(dmod), ptr(dmod[:, d:]), 2 * d,
-         ptr(ypre), stream())
+         ptr(ypre), 0, stream())
     return dx, dmod
 
 
-def gate_bwd(dout, y, g, tpf, want_bias=True):
-    """-> dy [T, d] bf16, dg [F, d] fp32, per-frame bias partials [F, d] fp32 (or None)."""
+def adaln_bwd_into(dy, x, rstd, scale, tpf, dmod, dres=None, ypre=None):
+    """adaln_bwd writing [dscale | dshift] as bf16 straight into dmod (a [F, 2d] bf16 view of a
+    modulation-gradient matrix, any row stride) -> dx [T, d] bf16."""
+    T, d = x.shape
+    assert dmod.dtype == BF16 and dmod.shape == (T // tpf, 2 * d) and dmod.stride(1) == 1
+    dx = torch.empty(T, d, device=x.device, dtype=BF16)
+    call("owlk_adaln_bwd", ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(rstd), ptr(scale), scale.stride(0), tpf,
+         T, d, ptr(dres), dres.stride(0) if dres is not None else 0, ptr(dx), d, ptr(dmod), ptr(dmod[:, d:]),
+         dmod.stride(0), ptr(ypre), 1, stream())
+    return dx
+
+
+def gate_bwd(dout, y, g, tpf, want_bias=True, dg_out=None):
+    """-> dy [T, d] bf16, dg [F, d] fp32 (or written as bf16 into dg_out, a [F, d] bf16 view of a
+    modulation-gradient matrix), per-frame bias partials [F, d] fp32 (or None)."""
     T, d = y.shape
     F_ = T // tpf
     dy = torch.empty(T, d, device=y.device, dtype=BF16)
-    dg = torch.empty(F_, d, device=y.device, dtype=F32)
+    if dg_out is None:
+        dg = torch.empty(F_, d, device=y.device, dtype=F32)
+    else:
+        assert dg_out.dtype == BF16 and dg_out.shape == (F_, d) and dg_out.stride(1) == 1
+        dg = dg_out
     dbf = torch.empty(F_, d, device=y.device, dtype=F32) if want_bias else None
     call("owlk_gate_bwd", ptr(dout), dout.stride(0), ptr(y), y.stride(0), ptr(g), g.stride(0), tpf, T, d, ptr(dy), d,
-         ptr(dg), ptr(dbf), d, stream())
+         ptr(dg), dg.stride(0), int(dg.dtype == BF16), ptr(dbf), d, stream())
     return dy, dg, dbf
 
 
@@ -475,13 +492,27 @@ def unpatchify(tok, B, N, C, h, w):
 
 
 def mse(pred, tgt, want_grad=True, grad_scale=1.0):
-    """F.mse_loss (fp32 math on bf16 inputs) + d loss / d pred (bf16)."""
+    """F.mse_loss (fp32 math on bf16 inputs; fp32 0-dim loss) + d loss / d pred (bf16)."""
     n = pred.numel()
     nb = 1024
     partial = torch.empty(nb, device=pred.device, dtype=F32)
+    loss = torch.empty((), device=pred.device, dtype=F32)
     dpred = torch.empty_like(pred) if want_grad else None
-    call("owlk_mse", ptr(pred), ptr(tgt), n, float(2.0 * grad_scale / n), ptr(dpred), ptr(partial), nb, stream())
-    return partial.double().sum().float() / n, dpred
+    call("owlk_mse", ptr(pred), ptr(tgt), n, float(2.0 * grad_scale / n), ptr(dpred), ptr(partial), nb, ptr(loss),
+         stream())
+    return loss, dpred
+
+
+def mse_grad(pred, tgt, gout=None):
+    """backward of F.mse_loss(pred, tgt): bf16((2 / n (pred - tgt)) gout), gout a device fp32 scalar."""
+    assert pred.is_contiguous() and tgt.is_contiguous() and pred.dtype == tgt.dtype == BF16
+    if gout is not None:
+        gout = gout.to(F32).contiguous() if gout.dtype != F32 else gout.contiguous()
+        assert gout.numel() == 1
+    dpred = torch.empty_like(pred)
+    n = pred.numel()
+    call("owlk_mse_grad", ptr(pred), ptr(tgt), n, float(2.0 / n), ptr(gout), ptr(dpred), stream())
+    return dpred
 
 
 def colsum(x, out=None):
@@ -664,3 +695,91 @@ def layernorm_bwd(dy, x, mean, rstd):
     call("owlk_layernorm_bwd", ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), T, d, ptr(dx),
          dx.stride(0), stream(), key="layernorm_bwd")
     return dx
+
+
+def _in_dtype_flag(t, name):
+    assert t.dtype in (BF16, F32), f"{name}: bf16 or fp32 input expected (got {t.dtype})"
+    return int(t.dtype == F32)
+
+
+def cond_embed(R, ts=None, tfreq=None, tmult=1000.0, mouse=None, mfreq=None, mmult=1000.0, wang=None, btn=None,
+               nbp=0):
+    """owlk_cond_embed over R frame rows -> (ts_in [R, 2 ht], mouse_in [R, 4 hm], ang [R, 2], btn_in [R, nbp]),
+    bf16 (None where the input is None).  ts [R], mouse [R, 2] (any row stride), btn [R, nb] (row stride),
+    bf16 or fp32; tfreq / mfreq fp32 [ht] / [hm]; wang the angle_proj weight fp32 [2 hm, 2]."""
+    dev = (ts if ts is not None else mouse if mouse is not None else btn).device
+    ts_in = mouse_in = ang = btn_in = None
+    ht = hm = nb = 0
+    ldm = ldb = 0
+    if ts is not None:
+        assert ts.numel() == R and ts.is_contiguous() and tfreq.dtype == F32 and tfreq.is_contiguous()
+        ht = tfreq.numel()
+        ts_in = torch.empty(R, 2 * ht, device=dev, dtype=BF16)
+    if mouse is not None:
+        assert mouse.dim() == 2 and mouse.shape == (R, 2) and mouse.stride(1) == 1
+        assert mfreq.dtype == F32 and mfreq.is_contiguous() and wang.dtype == F32 and wang.is_contiguous()
+        hm = mfreq.numel()
+        assert wang.shape == (2 * hm, 2)
+        ldm = mouse.stride(0)
+        mouse_in = torch.empty(R, 4 * hm, device=dev, dtype=BF16)
+        ang = torch.empty(R, 2, device=dev, dtype=BF16)
+    if btn is not None:
+        assert btn.dim() == 2 and btn.shape[0] == R and btn.stride(1) == 1
+        nb, ldb = btn.shape[1], btn.stride(0)
+        assert nbp >= nb
+        btn_in = torch.empty(R, nbp, device=dev, dtype=BF16)
+    call("owlk_cond_embed", ptr(ts), _in_dtype_flag(ts, "ts") if ts is not None else 0, ptr(tfreq), ht,
+         float(tmult), ptr(ts_in), 2 * ht, ptr(mouse), _in_dtype_flag(mouse, "mouse") if mouse is not None else 0,
+         ldm, ptr(mfreq), hm, float(mmult), ptr(wang), ptr(mouse_in), 4 * hm, ptr(ang), ptr(btn),
+         _in_dtype_flag(btn, "btn") if btn is not None else 0, ldb, nb, nbp, ptr(btn_in), nbp, R, stream())
+    return ts_in, mouse_in, ang, btn_in
+
+
+def cond_silu_fwd(t, m=None, b=None, hc=None, rows_per=1, keep_cond=True):
+    """cond = t + (hc ? m + b : 0) (bf16 adds), s = silu(cond): -> (cond or None, s), [R, d] bf16.
+    hc: bool [R / rows_per] (has_controls per sample) or None."""
+    R, d = t.shape
+    for x in (t, m, b):
+        assert x is None or (x.shape == (R, d) and x.is_contiguous() and x.dtype == BF16)
+    if hc is not None:
+        assert hc.dtype == torch.bool and hc.is_contiguous() and hc.numel() * rows_per == R
+    cond = torch.empty_like(t) if keep_cond and m is not None else (t if keep_cond else None)
+    s = torch.empty_like(t)
+    call("owlk_cond_silu_fwd", ptr(t), ptr(m), ptr(b), ptr(hc), rows_per, R, d,
+         ptr(cond) if cond is not t else None, ptr(s), stream())
+    return cond, s
+
+
+def cond_silu_bwd(ds, cond=None, hc=None, rows_per=1, want_cond=True, want_ctrl=False):
+    """ds [R, d] (fp32, or bf16) -> (dcond, dctrl) bf16: dcond = bf16(ds) silu'(cond), or ds itself
+    when cond is None (then dcond is only returned, not written); dctrl = hc ? dcond : 0.  Either
+    is None when not wanted."""
+    R, d = ds.shape
+    assert ds.dtype in (F32, BF16) and ds.is_contiguous()
+    assert cond is None or (cond.shape == (R, d) and cond.is_contiguous() and cond.dtype == BF16)
+    if hc is not None:
+        assert hc.dtype == torch.bool and hc.is_contiguous() and hc.numel() * rows_per == R
+    if cond is None:
+        assert ds.dtype == BF16
+        dcond = ds if want_cond else None
+    else:
+        dcond = torch.empty(R, d, device=ds.device, dtype=BF16) if want_cond else None
+    dctrl = torch.empty(R, d, device=ds.device, dtype=BF16) if want_ctrl else None
+    call("owlk_cond_silu_bwd", ptr(ds), int(ds.dtype == BF16), ptr(cond), ptr(hc), rows_per, R, d,
+         ptr(dcond) if cond is not None else None, ptr(dctrl), stream())
+    return dcond, dctrl
+
+
+def small_k_wgrad(dy, x, K_, out=None, beta=0.0):
+    """fp32 dW[n, k] = beta dW + sum_r dy[r, n] x[r, k] for k < K_ <= 16 (x may be wider: its first K_
+    columns are used); out: [N, K_] fp32 (row stride any)."""
+    R, N = dy.shape
+    assert dy.stride(1) == 1 and x.stride(1) == 1 and x.shape[0] == R and x.shape[1] >= K_
+    assert dy.dtype == BF16 and x.dtype == BF16
+    if out is None:
+        out = torch.empty(N, K_, device=dy.device, dtype=F32)
+        beta = 0.0
+    assert out.shape == (N, K_) and out.dtype == F32 and out.stride(1) == 1
+    call("owlk_small_k_wgrad", ptr(dy), dy.stride(0), ptr(x), x.stride(0), R, N, K_, ptr(out), out.stride(0),
+         float(beta), stream())
+    return out

@@ -3,6 +3,7 @@ import torch
 from torch import nn
 
 from ..nn.attn import DiT, FinalLayer
+from ..nn.cond import conditioning
 from ..nn.embeddings import TimestepEmbedding
 from ..nn.fused import linear
 from .flow import TorchNoise, flow_loss, noised_tokens
@@ -20,10 +21,10 @@ class AudioRFTCore(nn.Module):
         assert config.tokens_per_frame == 1
 
     def forward(self, x, t, doc_id=None, kv_cache=None, local_block_mask=None, global_block_mask=None):
-        t_cond = self.t_embed(t)
+        s = conditioning(self, t, want="s")  # silu(t_embed(t)) (unconditional: cond = t_embed(t))
         h = linear(x, self.proj_in.weight)
-        h = self.transformer(h, t_cond, doc_id, kv_cache, local_block_mask, global_block_mask)
-        return self.proj_out(h, t_cond)
+        h = self.transformer(h, None, doc_id, kv_cache, local_block_mask, global_block_mask, scond=s)
+        return self.proj_out(h, None, scond=s)
 
 
 class AudioRFT(nn.Module):

@@ -10,6 +10,7 @@ from torch import nn
 
 from .. import kernels as K
 from ..nn.attn import DiT, FinalLayer
+from ..nn.cond import conditioning
 from ..nn.embeddings import ControlEmbedding, TimestepEmbedding
 from ..nn.fused import linear
 from .flow import TorchNoise, flow_loss, handle_cfg, noised_tokens
@@ -30,21 +31,18 @@ class GameRFTCore(nn.Module):
         self.uncond = config.uncond
 
     def cond(self, t, mouse, btn, has_controls=None):
-        t_cond = self.t_embed(t)
-        if self.uncond:
-            return t_cond
-        ctrl = self.control_embed(mouse, btn)
-        if has_controls is not None:
-            ctrl = torch.where(has_controls[:, None, None], ctrl, torch.zeros_like(ctrl))
-        return t_cond + ctrl
+        """gamerft.py:39-48: t_embed(t) + (has_controls ? control_embed(mouse, btn) : 0), bf16 [B, n, d]
+        (one fused conditioning pass, nn/cond.py)."""
+        return conditioning(self, t, mouse, btn, has_controls, want="cond")
 
     def forward_tokens(self, x_tok, t, mouse, btn, doc_id=None, has_controls=None, kv_cache=None,
                        local_block_mask=None, global_block_mask=None):
-        """x_tok [B, n*h*w, C] -> velocity tokens [B, n*h*w, C] (bf16)."""
-        cond = self.cond(t, mouse, btn, has_controls)
+        """x_tok [B, n*h*w, C] -> velocity tokens [B, n*h*w, C] (bf16).  Every consumer of cond
+        reads silu(cond), so the conditioning pass hands out s = silu(cond) directly."""
+        s = conditioning(self, t, mouse, btn, has_controls, want="s")
         x = linear(x_tok, self.proj_in.weight)
-        x = self.transformer(x, cond, doc_id, kv_cache, local_block_mask, global_block_mask)
-        return self.proj_out(x, cond)
+        x = self.transformer(x, None, doc_id, kv_cache, local_block_mask, global_block_mask, scond=s)
+        return self.proj_out(x, None, scond=s)
 
     def forward(self, x, t, mouse, btn, doc_id=None, has_controls=None, kv_cache=None, local_block_mask=None,
                 global_block_mask=None):

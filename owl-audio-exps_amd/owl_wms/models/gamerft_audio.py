@@ -13,6 +13,7 @@ from torch import nn
 
 from .. import kernels as K
 from ..nn.attn import DiT, FinalLayer
+from ..nn.cond import conditioning
 from ..nn.embeddings import ControlEmbedding, TimestepEmbedding
 from ..nn.fused import linear
 from ..nn.mmattn import MMDIT
@@ -44,13 +45,8 @@ class GameRFTAudioCore(nn.Module):
         self.uncond = config.uncond
 
     def cond(self, t, mouse, btn, has_controls=None):
-        t_cond = self.t_embed(t)
-        if self.uncond:
-            return t_cond
-        ctrl = self.control_embed(mouse, btn)
-        if has_controls is not None:
-            ctrl = torch.where(has_controls[:, None, None], ctrl, torch.zeros_like(ctrl))
-        return t_cond + ctrl
+        """gamerft_audio.py: t_embed(t) + (has_controls ? control_embed(mouse, btn) : 0) (nn/cond.py)."""
+        return conditioning(self, t, mouse, btn, has_controls, want="cond")
 
     def forward_tokens(self, xv, xa, t, mouse, btn, has_controls=None, kv_cache=None):
         """xv [B, n*h*w, C] video tokens, xa [B, n, Ca] -> (video [B, n*h*w, C], audio [B, n, Ca])."""

@@ -10,13 +10,13 @@ semantics (attn.py:86-107): cached K/V prepended, local layers keep the last
 ``local_window * tokens_per_frame`` keys when decoding unmasked.
 """
 import torch
-import torch.nn.functional as F
 import weakref
 from torch import nn
 from torch.utils.checkpoint import checkpoint as torch_checkpoint
 
 from .. import kernels as K
-from .fused import BlockGeometry, DiTBlockFn, ModFn, adaln, bf16_weight, linear, stacked_modulation_weights
+from .fused import (BlockGeometry, DiTBlockFn, ModFn, adaln_mod, bf16_weight, cond_silu, linear,
+                    stacked_modulation_weights)
 from .mlp import MLP
 from .modulation import AdaLN, Gate
 from .rope import get_rope_cls
@@ -154,7 +154,7 @@ class DiTBlock(nn.Module):
         ws, bs = self.mod_params()
         params = [t for pair in zip(ws, bs) for t in pair]
         W, bvec = stacked_modulation_weights(self, params)
-        return ModFn.apply(F.silu(cond), W, bvec, *params)
+        return ModFn.apply(cond_silu(cond), W, bvec, *params)
 
     def mod_params(self):
         """(weights, biases) of the four per-frame modulation Linears, in the column order of
@@ -162,30 +162,38 @@ class DiTBlock(nn.Module):
         fcs = (self.adaln1.fc, self.gate1.fc_c, self.adaln2.fc, self.gate2.fc_c)
         return [f.weight for f in fcs], [f.bias for f in fcs]
 
-    def forward(self, x, cond, block_mask, kv_cache=None, mods=None):
+    def forward(self, x, cond, block_mask, kv_cache=None, mods=None, scond=None):
+        """scond: silu(cond) from fused.cond_silu / cond.CondFn (computed here when not given)."""
         if kv_cache is not None:
             with torch.no_grad():
-                return self._forward_cached(x, cond, block_mask, kv_cache, mods)
+                return self._forward_cached(x, cond, block_mask, kv_cache, mods, scond)
         cfg = self.config
-        ab1, g1, ab2, g2 = self.modulation(cond)
+        if scond is None:
+            scond = cond_silu(cond)
+        ws, bs = self.mod_params()
+        mparams = [t for pair in zip(ws, bs) for t in pair]
+        W, bvec = stacked_modulation_weights(self, mparams)
         H = cfg.n_heads
         rope = self.attn.rope
         geo = BlockGeometry(H, cfg.d_model // H, cfg.tokens_per_frame, block_mask, rope.cos, rope.sin, 0,
                             keep_attn=id(self) if getattr(self, "_checkpointed", False) else None)
         a, m = self.attn, self.mlp
-        return DiTBlockFn.apply(x.to(torch.bfloat16).contiguous(), ab1, g1, ab2, g2, a.qkv.weight, a.qkv.bias,
-                                a.out.weight, a.out.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias, geo)
+        return DiTBlockFn.apply(x.to(torch.bfloat16).contiguous(), scond, W, bvec, geo, a.qkv.weight, a.qkv.bias,
+                                a.out.weight, a.out.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias,
+                                *mparams)
 
-    def _forward_cached(self, x, cond, block_mask, kv_cache, mods=None):
+    def _forward_cached(self, x, cond, block_mask, kv_cache, mods=None, scond=None):
         """No-grad forward of the decode path (attn.py:86-107 cache branch).  mods: this block's
         [rows, 6d] column slice of DiT._decode_modulation, else computed here."""
         cfg = self.config
         d, tpf = cfg.d_model, cfg.tokens_per_frame
         B, L, _ = x.shape
         if mods is None:
-            ab1, g1, ab2, g2 = self.modulation(cond)
-        else:
-            ab1, g1, ab2, g2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
+            ws, bs = self.mod_params()
+            W, bvec = stacked_modulation_weights(self, [t for pair in zip(ws, bs) for t in pair])
+            s = scond if scond is not None else cond_silu(cond)
+            mods = K.gemm(s.reshape(-1, d).to(torch.bfloat16).contiguous(), W, bias=bvec)
+        ab1, g1, ab2, g2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
         xx = x.reshape(B * L, d).to(torch.bfloat16).contiguous()
         ab1, ab2 = ab1.reshape(-1, 2 * d), ab2.reshape(-1, 2 * d)
         h1, _ = K.adaln_fwd(xx, ab1[:, :d], ab1[:, d:], tpf)
@@ -222,7 +230,11 @@ class DiT(nn.Module):
         return get_block_mask(seq_len + q_offset, self.config.tokens_per_frame, window_len, doc_id, q_offset,
                               self.config.causal, device)
 
-    def forward(self, x, cond, doc_id=None, kv_cache=None, local_block_mask=None, global_block_mask=None):
+    def forward(self, x, cond, doc_id=None, kv_cache=None, local_block_mask=None, global_block_mask=None,
+                scond=None):
+        """scond: silu(cond) as produced by cond.CondFn (GameRFTCore) -- every block's modulation reads
+        it and sums its gradient into one fp32 accumulator (fused.CondGrad); computed here from cond
+        when not given."""
         seq_len, device = x.size(1), x.device
         q_offset = kv_cache.length_at(0) if kv_cache is not None else 0
         if local_block_mask is None and not self.decoding:
@@ -234,7 +246,9 @@ class DiT(nn.Module):
         # optional: checkpoint only the first `checkpoint_layers` blocks and keep the rest's activations
         # (HBM headroom on a 288 GB MI355X trades for the recompute); default = every block, as the reference
         n_ck = getattr(self.config, "checkpoint_layers", None)
-        mods = self._decode_modulation(cond) if kv_cache is not None else None
+        if scond is None:
+            scond = cond_silu(cond)
+        mods = self._decode_modulation(scond) if kv_cache is not None else None
         d6 = 6 * self.config.d_model
         for i, block in enumerate(self.blocks):
             mask = local_block_mask if self.local_layers[i] else global_block_mask
@@ -243,21 +257,22 @@ class DiT(nn.Module):
                 continue
             ck = ckpt and (n_ck is None or i < n_ck)
             block._checkpointed = ck  # the re-run inside backward reuses the kept attention output
-            x = checkpoint(block, x, cond, mask, kv_cache) if ck else block(x, cond, mask, kv_cache)
+            x = checkpoint(block, x, cond, mask, kv_cache, None, scond) if ck else \
+                block(x, cond, mask, kv_cache, None, scond)
         if kv_cache is not None and kv_cache.should_update and getattr(kv_cache, "dev", None) is not None:
             kv_cache.sync_device_state()  # every layer committed the frame
         return x
 
     @torch.no_grad()
-    def _decode_modulation(self, cond):
+    def _decode_modulation(self, scond):
         """Every block's per-frame modulation (DiTBlock.modulation) for a no-grad KV-cache forward
-        as ONE GEMM: silu(cond) [rows, d] against all blocks' modulation weights stacked
+        as ONE GEMM: scond = silu(cond) [rows, d] against all blocks' modulation weights stacked
         [L x 6d, d].  Decode has 1-2 rows per call, so the 4 x L per-block GEMMs were each a
         latency-bound launch pair; the stacked GEMM streams the same 28 MB/block of weights once.
         The bf16 stack is rebuilt when any of its parameters changes (version counters)."""
         ws, bs = zip(*(b.mod_params() for b in self.blocks))
         ws, bs = [w for g in ws for w in g], [b for g in bs for b in g]
-        key = (cond.device,) + tuple(p._version for p in ws + bs) + tuple(id(p) for p in ws)
+        key = (scond.device,) + tuple(p._version for p in ws + bs) + tuple(id(p) for p in ws)
         ent = getattr(self, "_mod_stack", None)
         if ent is None or ent[0] != key:
             W = torch.cat([w.detach().to(torch.bfloat16) for w in ws]).contiguous()
@@ -265,8 +280,7 @@ class DiT(nn.Module):
             ent = (key, W, bias)
             object.__setattr__(self, "_mod_stack", ent)
         d = self.config.d_model
-        s = F.silu(cond.reshape(-1, d)).to(torch.bfloat16).contiguous()
-        return K.gemm(s, ent[1], bias=ent[2])
+        return K.gemm(scond.reshape(-1, d).to(torch.bfloat16).contiguous(), ent[1], bias=ent[2])
 
 
 class FinalLayer(nn.Module):
@@ -278,5 +292,8 @@ class FinalLayer(nn.Module):
         self.act = nn.SiLU()
         self.proj = nn.Linear(d_model, channels * patch_size * patch_size)
 
-    def forward(self, x, cond):
-        return linear(self.norm(x, cond, act=True), self.proj.weight, self.proj.bias)
+    def forward(self, x, cond, scond=None):
+        """scond: silu(cond) (fused.cond_silu / cond.CondFn), computed here when not given."""
+        s = scond if scond is not None else cond_silu(cond)
+        h = adaln_mod(x, s, self.norm.fc.weight, self.norm.fc.bias, x.shape[1] // s.shape[1], act=True)
+        return linear(h, self.proj.weight, self.proj.bias)

@@ -169,6 +169,130 @@ def adaln(x, scale, shift, tpf, act=False):
     return AdaLNFn.apply(x, scale, shift, tpf, act)
 
 
+class CondGrad:
+    """The gradient of s = silu(cond), summed over every consumer of s in fp32.
+
+    s feeds one GEMM per DiT block (the stacked modulation fc's) and the final layer's AdaLN fc.
+    Under autograd each would hand back a bf16 [F, d] gradient and the engine would add them one
+    by one (bf16 adds).  Instead each consumer's backward runs its dX GEMM with beta = 1 onto this
+    accumulator and returns None for s; the producer of s (CondSiluFn / cond.CondFn) reads the sum
+    in its own backward, which autograd runs after every consumer's.  Consumers find the
+    accumulator on s (attribute ``_owl_cond_grad``, set by the producer's wrapper)."""
+
+    __slots__ = ("ds",)
+
+    def __init__(self):
+        self.ds = None
+
+    def take(self, g, shape):
+        """the accumulated fp32 sum (+ g, a gradient some consumer returned through autograd) as
+        [F, d] fp32, or None; the accumulator is emptied."""
+        ds, self.ds = self.ds, None
+        if g is not None:  # a consumer outside the fused path (reference-API callers)
+            g = g.reshape(-1, shape[-1]).float()
+            ds = g if ds is None else ds + g
+        return ds
+
+
+def cond_grad_of(s):
+    return getattr(s, "_owl_cond_grad", None)
+
+
+def cond_grad_add(cg, dm, w, shape):
+    """consumer side of CondGrad: ds = dm w (dm [F, N] bf16 rows, any stride; w [N, d] bf16).  Added
+    onto the accumulator (returns None) or, with none, returned as the bf16 gradient of s."""
+    if cg is None:
+        return K.gemm(dm, w, b_trans=True).view(shape)
+    if cg.ds is None:
+        cg.ds = K.gemm(dm, w, b_trans=True, out_f32=True)
+    else:
+        K.gemm(dm, w, b_trans=True, out=cg.ds, out_f32=True, beta=1.0)
+    return None
+
+
+class CondSiluFn(torch.autograd.Function):
+    """s = silu(cond) (bf16, owlk_cond_silu_fwd) for callers that hold cond itself (DiT / FinalLayer /
+    AdaLN called with the reference signature); its consumers accumulate into a CondGrad."""
+
+    @staticmethod
+    def forward(ctx, cond, cg):
+        ctx.set_materialize_grads(False)
+        shp = cond.shape
+        c2 = cond.reshape(-1, shp[-1]).to(BF16).contiguous()
+        _, s = K.cond_silu_fwd(c2)
+        ctx.save_for_backward(c2)
+        ctx.cg, ctx.shp, ctx.cdtype = cg, shp, cond.dtype
+        return s.view(shp)
+
+    @staticmethod
+    def backward(ctx, g):
+        (c2,) = ctx.saved_tensors
+        ds = ctx.cg.take(g, ctx.shp)
+        if ds is None:
+            return None, None
+        dc, _ = K.cond_silu_bwd(ds.contiguous(), c2)
+        return dc.view(ctx.shp).to(ctx.cdtype), None
+
+
+def cond_silu(cond):
+    """silu(cond) as bf16 carrying a CondGrad (see CondGrad); a tensor that already is such an s
+    (``_owl_cond_grad`` set) is returned as is."""
+    if cond_grad_of(cond) is not None:
+        return cond
+    if not (torch.is_grad_enabled() and cond.requires_grad):
+        return K.cond_silu_fwd(cond.reshape(-1, cond.shape[-1]).to(BF16).contiguous(),
+                               keep_cond=False)[1].view(cond.shape)
+    cg = CondGrad()
+    s = CondSiluFn.apply(cond, cg)
+    s._owl_cond_grad = cg
+    return s
+
+
+class AdaLNModFn(torch.autograd.Function):
+    """AdaLN with its modulation Linear (modulation.py:7-25; FinalLayer attn.py:264-277):
+    [scale | shift] = s W^T + b (one GEMM on s = silu(cond)), y = AdaLN(x) (optionally -> silu(y)).
+    Backward: d[scale | shift] lands bf16 in one [F, 2d] matrix (owlk_adaln_bwd, mod_bf16), whose
+    dX GEMM goes onto the CondGrad of s and whose dW / db go into the parameters' bucket views."""
+
+    @staticmethod
+    def forward(ctx, x, s, w, b, tpf, act):
+        shp = x.shape
+        d = shp[-1]
+        s2 = s.reshape(-1, d).to(BF16).contiguous()
+        wb = bf16_weight(w)
+        ab = K.gemm(s2, wb, bias=b)
+        x2 = x.reshape(-1, d).to(BF16).contiguous()
+        if act:
+            y, rstd, ya = K.adaln_fwd(x2, ab[:, :d], ab[:, d:], tpf, act=True)
+        else:
+            (y, rstd), ya = K.adaln_fwd(x2, ab[:, :d], ab[:, d:], tpf), None
+        ctx.save_for_backward(x2, rstd, ab, y if act else None, s2, w)
+        ctx.tpf, ctx.shp, ctx.act, ctx.sshape, ctx.b = tpf, shp, act, s.shape, b
+        ctx.cg = cond_grad_of(s)
+        return (ya if act else y).view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, rstd, ab, ypre, s2, w = ctx.saved_tensors
+        d = x2.shape[1]
+        dy2 = dy.reshape(-1, d).to(BF16).contiguous()
+        dab = torch.empty_like(ab)
+        dx = K.adaln_bwd_into(dy2, x2, rstd, ab[:, :d], ctx.tpf, dab, ypre=ypre if ctx.act else None)
+        ds = dw = db = None
+        if ctx.needs_input_grad[1]:
+            ds = cond_grad_add(ctx.cg, dab, bf16_weight(w), ctx.sshape)
+        if ctx.needs_input_grad[2]:
+            dw = wgrad_into(w, dab, s2)
+        if ctx.b is not None and ctx.needs_input_grad[3]:
+            db = bgrad_into(ctx.b, dab)
+        return dx.view(ctx.shp), ds, dw, db, None, None
+
+
+def adaln_mod(x, s, w, b, tpf, act=False):
+    """AdaLN(x) with [scale | shift] = s W^T + b; s = cond_silu(cond)."""
+    return AdaLNModFn.apply(x, s, w, b, tpf, act)
+
+
 class BlockGeometry:
     """Static per-forward data of a DiT block: heads, frame mask, RoPE tables; keep_attn = a key
     per block when the block runs under activation checkpointing (see _ATTN_KEEP)."""
@@ -201,14 +325,20 @@ def _keep_attention(geo, x, wqkv, o, lse):
 
 
 class DiTBlockFn(torch.autograd.Function):
+    """One DiTBlock with its modulation: mods = s Wmod^T + bmod ([F, 6d], s = silu(cond), the four
+    modulation fc's stacked, see stacked_modulation_weights) as the block's first GEMM; the
+    backward writes d mods bf16 straight into one [F, 6d] matrix (adaln / gate backward kernels),
+    runs its dX GEMM onto the CondGrad of s and the four dW / db into the bucket views."""
+
     @staticmethod
-    def forward(ctx, x, ab1, g1, ab2, g2, wqkv, bqkv, wout, bout, w1, b1, w2, b2, geo):
+    def forward(ctx, x, s, wmod, bmod, geo, wqkv, bqkv, wout, bout, w1, b1, w2, b2, *mparams):
         B, T, d = x.shape
         M = B * T
         H, D, tpf = geo.H, geo.D, geo.tpf
         xx = x.reshape(M, d)
-        a1, a2 = ab1.reshape(-1, 2 * d), ab2.reshape(-1, 2 * d)
-        gg1, gg2 = g1.reshape(-1, d), g2.reshape(-1, d)
+        s2 = s.reshape(-1, d).to(BF16).contiguous()
+        mods = K.gemm(s2, wmod, bias=bmod)
+        a1, gg1, a2, gg2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
 
         h1, r1 = K.adaln_fwd(xx, a1[:, :d], a1[:, d:], tpf)
         qkv = K.gemm(h1, bf16_weight(wqkv), bias=bqkv)
@@ -230,26 +360,29 @@ class DiTBlockFn(torch.autograd.Function):
         y2 = torch.empty(M, d, device=x.device, dtype=BF16)
         out = K.gemm(a, bf16_weight(w2), bias=b2, epi=K.EPI_GATE_RESID, aux=y2, gate=gg2, tpf=tpf, resid=x1)
 
-        ctx.save_for_backward(xx, a1, gg1, a2, gg2, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2,
+        ctx.save_for_backward(xx, s2, wmod, mods, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2,
                               r2, a_pre, a, y2)
-        ctx.geo, ctx.shape = geo, (B, T, d)
-        ctx.params = (wqkv, bqkv, wout, bout, w1, b1, w2, b2)
+        ctx.geo, ctx.shape, ctx.sshape = geo, (B, T, d), s.shape
+        ctx.params = (wqkv, bqkv, wout, bout, w1, b1, w2, b2) + tuple(mparams)
+        ctx.cg = cond_grad_of(s)
         return out.view(B, T, d)
 
     @staticmethod
     def backward(ctx, dout):
-        (xx, a1, gg1, a2, gg2, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2, r2, a_pre, a,
+        (xx, s2, wmod, mods, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2, r2, a_pre, a,
          y2) = ctx.saved_tensors
         geo = ctx.geo
         B, T, d = ctx.shape
         M = B * T
         H, D, tpf = geo.H, geo.D, geo.tpf
+        a1, gg1, a2, gg2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
         dx2 = dout.reshape(M, d).to(BF16).contiguous()
+        dm = torch.empty_like(mods)  # d mods, bf16 as the modulation Linears' output gradient
 
-        prm = ctx.params  # (wqkv, bqkv, wout, bout, w1, b1, w2, b2) Parameters: direct gradient sinks
+        prm = ctx.params  # (wqkv, bqkv, wout, bout, w1, b1, w2, b2, 4 x (w, b) mod) Parameters: gradient sinks
 
         # ---- MLP branch
-        dy2, dg2, dbf2 = K.gate_bwd(dx2, y2, gg2, tpf)
+        dy2, _, dbf2 = K.gate_bwd(dx2, y2, gg2, tpf, dg_out=dm[:, 5 * d:])
         db2 = bgrad_into(prm[7], dbf2)  # per-frame partials [F, d] -> bias gradient
         sink_b1 = grad_sink(prm[5])
         db1 = sink_b1 if sink_b1 is not None else torch.zeros(a_pre.shape[1], device=a_pre.device,
@@ -262,11 +395,11 @@ class DiTBlockFn(torch.autograd.Function):
         dw1 = wgrad_into(prm[4], dapre, h2)
         dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
         del dapre
-        dx1, dmod2 = K.adaln_bwd(dh2, x1, r2, a2[:, :d], tpf, dres=dx2)
+        dx1 = K.adaln_bwd_into(dh2, x1, r2, a2[:, :d], tpf, dm[:, 3 * d:5 * d], dres=dx2)
         del dh2
 
         # ---- attention branch
-        dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf)
+        dy1, _, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf, dg_out=dm[:, 2 * d:3 * d])
         dbout = bgrad_into(prm[3], dbf1)
         do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
         dwout = wgrad_into(prm[2], dy1, o)
@@ -290,12 +423,24 @@ class DiTBlockFn(torch.autograd.Function):
         dwqkv = wgrad_into(prm[0], dqkv, h1)
         dh1 = K.gemm(dqkv, bf16_weight(wqkv), b_trans=True)
         del dqkv
-        dx, dmod1 = K.adaln_bwd(dh1, xx, r1, a1[:, :d], tpf, dres=dx1)
+        dx = K.adaln_bwd_into(dh1, xx, r1, a1[:, :d], tpf, dm[:, :2 * d], dres=dx1)
+        del dh1
 
-        nf = M // tpf
-        return (dx.view(B, T, d), dmod1.view(B, nf // B, 2 * d), dg1.view(B, nf // B, d),
-                dmod2.view(B, nf // B, 2 * d), dg2.view(B, nf // B, d),
-                dwqkv, dbqkv, dwout, dbout, dw1, db1, dw2, db2, None)
+        # ---- modulation: one dX GEMM against the stack onto the CondGrad of s; dW / db per fc
+        ds = cond_grad_add(ctx.cg, dm, wmod, ctx.sshape) if ctx.needs_input_grad[1] else None
+        mgrads = []
+        for i, (lo, hi) in enumerate(_MOD_COLS(d)):
+            w, bias = prm[8 + 2 * i], prm[9 + 2 * i]
+            dmi = dm[:, lo:hi]
+            mgrads.append(wgrad_into(w, dmi, s2) if ctx.needs_input_grad[13 + 2 * i] else None)
+            mgrads.append(bgrad_into(bias, dmi) if ctx.needs_input_grad[14 + 2 * i] else None)
+        return (dx.view(B, T, d), ds, None, None, None,
+                dwqkv, dbqkv, dwout, dbout, dw1, db1, dw2, db2, *mgrads)
+
+
+def _MOD_COLS(d):
+    """column ranges of the stacked modulation output: adaln1 [2d] | gate1 [d] | adaln2 [2d] | gate2 [d]"""
+    return ((0, 2 * d), (2 * d, 3 * d), (3 * d, 5 * d), (5 * d, 6 * d))
 
 
 class ModFn(torch.autograd.Function):
@@ -378,15 +523,18 @@ def layer_norm(x):
 
 
 class FlowLossFn(torch.autograd.Function):
-    """F.mse_loss(pred_tok, tgt_tok) with the gradient produced by the same kernel."""
+    """F.mse_loss(pred_tok, tgt_tok): the loss from one kernel pass (+ a fixed-order finish), the
+    gradient in the backward from pred and tgt, scaled by the incoming loss gradient on the device
+    (no host sync, no separate multiply)."""
 
     @staticmethod
     def forward(ctx, pred, tgt):
-        loss, dpred = K.mse(pred.contiguous(), tgt.contiguous(), want_grad=pred.requires_grad)
-        ctx.save_for_backward(dpred)
+        pred, tgt = pred.contiguous(), tgt.contiguous()
+        loss, _ = K.mse(pred, tgt, want_grad=False)
+        ctx.save_for_backward(pred, tgt)
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        (dpred,) = ctx.saved_tensors
-        return dpred * g.to(dpred.dtype), None
+        pred, tgt = ctx.saved_tensors
+        return K.mse_grad(pred, tgt, g), None

@@ -1,8 +1,5 @@
 """mlp.py (reference: owl_wms/nn/mlp.py:6-37).  Same init, same state_dict keys (fc1, fc2)."""
-import torch.nn.functional as F
 from torch import nn
-
-from .fused import linear
 
 
 class MLPCustom(nn.Module):
@@ -18,9 +15,10 @@ class MLPCustom(nn.Module):
         nn.init.zeros_(self.fc2.bias)
 
     def forward(self, x):
-        # small per-frame MLPs (embeddings): two libowlk GEMMs around a bf16 SiLU
-        h = linear(x, self.fc1.weight, self.fc1.bias)
-        return linear(F.silu(h), self.fc2.weight, self.fc2.bias)
+        # fc1 GEMM with the SiLU epilogue, fc2 GEMM (cond.MLPFn); the conditioning MLPs of the
+        # training step run inside cond.CondFn instead
+        from .cond import mlp_custom
+        return mlp_custom(x, self)
 
 
 class MLP(MLPCustom):

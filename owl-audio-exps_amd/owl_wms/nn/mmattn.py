@@ -23,11 +23,10 @@ the cache is committed when updates are enabled, and the attention keeps the fra
 q_offset = the cached length (the reference's create_causal_block_mask(n_cached_tokens=offset)).
 """
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from .. import kernels as K
-from .fused import bf16_weight, linear
+from .fused import bf16_weight, cond_silu, linear
 from .mlp import MLP
 from .rope import get_rope_cls
 
@@ -340,7 +339,7 @@ class MMDIT(nn.Module):
         local_mask = self.get_block_mask(x0, x1, kv_cache, self.config.local_window)
         global_mask = self.get_block_mask(x0, x1, kv_cache, getattr(self.config, "global_window", None))
         lin = self.cond_proj[1]
-        c = linear(F.silu(cond), lin.weight, lin.bias)
+        c = linear(cond_silu(cond), lin.weight, lin.bias)
         cond0, cond1 = c.chunk(2, dim=-1)
         for i, block in enumerate(self.blocks):
             x0, x1 = block(x0, x1, cond0, cond1, local_mask if self.local_layers[i] else global_mask, kv_cache)

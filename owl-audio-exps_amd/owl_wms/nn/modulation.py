@@ -4,10 +4,9 @@ AdaLN / Gate keep the reference signature ``module(x, cond)``.  Inside DiTBlock 
 modulation vectors are computed once from silu(cond) and the modulate/gate math is fused into
 libowlk kernels (DiTBlockFn); these modules serve FinalLayer and any external caller.
 """
-import torch.nn.functional as F
 from torch import nn
 
-from .fused import adaln, linear
+from .fused import adaln, adaln_mod, cond_silu, linear
 
 
 class AdaLN(nn.Module):
@@ -20,9 +19,9 @@ class AdaLN(nn.Module):
         return linear(scond, self.fc.weight, self.fc.bias)
 
     def forward(self, x, cond, act=False):
-        b, n, d = cond.shape
-        ab = self.mod(F.silu(cond))
-        return adaln(x, ab[..., :d], ab[..., d:], x.shape[1] // n, act)
+        """AdaLN(x) with its fc on silu(cond), fused (fused.AdaLNModFn)."""
+        n = cond.shape[1]
+        return adaln_mod(x, cond_silu(cond), self.fc.weight, self.fc.bias, x.shape[1] // n, act)
 
 
 class Gate(nn.Module):
@@ -35,7 +34,7 @@ class Gate(nn.Module):
 
     def forward(self, x, cond):
         b, n, d = cond.shape
-        c = self.mod(F.silu(cond))
+        c = self.mod(cond_silu(cond))
         m = x.shape[1] // n
         return c[:, :, None, :].expand(b, n, m, d).reshape(b, n * m, d) * x
 
