@@ -207,6 +207,7 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="override n_frames (default: the config's)")
     ap.add_argument("--docs", type=int, default=1,
                     help="documents per packed sample (SURVEY §8(d) doc-mask variant: 4 x 384 frames)")
+    ap.add_argument("--lean", type=int, default=None, help="override model.lean_activations (0 / 1)")
     ap.add_argument("--ckpt-layers", type=int, default=None,
                     help="checkpoint only the first N blocks (configs with gradient_checkpointing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -248,6 +249,8 @@ def main():
     mc = cfg.model
     if args.ckpt_layers is not None:
         mc.checkpoint_layers = args.ckpt_layers
+    if args.lean is not None:
+        mc.lean_activations = bool(args.lean)
     if args.frames:
         mc.n_frames = args.frames
     tokens = mc.n_frames * mc.tokens_per_frame  # joint video + audio tokens for game_rft_audio
@@ -367,7 +370,7 @@ def main():
             for k, (n, ms_, fl_) in kernels[:40]:
                 log(f"  {k:60s} n={n:3d} {ms_:9.3f} ms  {fl_ / max(ms_, 1e-9) / 1e9:8.1f} TF/s")
             log(f"  total kernel time {tot_ms:.1f} ms")
-        log(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+    log(f"[bench] peak HBM allocated {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:

@@ -26,7 +26,8 @@ int owlk_device_ok(void);
  *   epi 0 STORE      C = alpha*acc + bf16(bias[n]) + beta*C           (bf16 or fp32 C)
  *       1 SILU       aux = bf16(acc + bias); C = bf16(silu(aux))
  *       2 GATE_RESID aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m / tpf, n] * y))
- *       3 DSILU      C = bf16(bf16(acc) * silu'(aux))
+ *       3 DSILU      C = bf16(bf16(acc) * silu'(aux)); a non-null resid is an OUTPUT here:
+ *                    resid = bf16(silu(aux)) (the activation a lean backward did not keep)
  *       4 AXPBY      C = bf16(bf16(alpha * bf16(acc)) + bf16(beta * aux))
  *       5 SCALE2     C = bf16(acc); aux = bf16(alpha * bf16(acc))   (a_trans = b_trans = 0 only)
  *   batch: blockIdx.z with element strides sA, sB, sC, sAux, sGate, sRes.
@@ -188,6 +189,10 @@ int owlk_flow_noise(const void* x, const void* z, const float* ts_raw, int C, in
                     void* tgt, float* ts_out, void* stream);
 /* token-major [BN*P, C] -> [BN, C, P] (gamerft.py:58) */
 int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out, void* stream);
+/* out = bf16(x + bf16(g[t / tpf] * y)), [T, d] bf16 rows: the GATE_RESID GEMM epilogue's output
+ * recomputed bit for bit from its kept inputs (residual x, gated branch y, per-frame gate g) */
+int owlk_gate_resid(const void* x, long ldx, const void* y, long ldy, const void* g, long ldg, long tpf, long T,
+                    int d, void* out, long ldo, void* stream);
 /* MSE (gamerft.py:111): partial[block] = sum (pred - tgt)^2; dpred (optional) = bf16(gscale * (pred - tgt));
  * loss (optional, fp32 scalar) = (float)(double sum of the partials in block order) / n */
 int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,

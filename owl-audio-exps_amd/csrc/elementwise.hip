@@ -478,6 +478,26 @@ __global__ __launch_bounds__(256) void unpatchify_k(const bf16* __restrict__ tok
   for (int i = threadIdx.x; i < C * P; i += 256) out[fr * (long)C * P + i] = (bf16)tile[(i / P) * (P + 1) + i % P];
 }
 
+// ------------------------------------------------------------------ gate + residual (recompute)
+// out = bf16(x + bf16(g[t / tpf] * y)): the GATE_RESID GEMM epilogue's output rebuilt from its
+// kept inputs (the lean block backward), bit for bit
+__global__ __launch_bounds__(256) void gate_resid_k(const bf16* __restrict__ x, long ldx, const bf16* __restrict__ y,
+                                                    long ldy, const bf16* __restrict__ g, long ldg, long tpf, long T,
+                                                    int d, bf16* __restrict__ out, long ldo) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int nch = d / 8;
+  if (idx >= T * nch) return;
+  const long t = idx / nch;
+  const int c = (int)(idx - t * nch) * 8;
+  float xv[8], yv[8], gv[8], o[8];
+  unpack8(*(const bf16x8*)(x + t * ldx + c), xv);
+  unpack8(*(const bf16x8*)(y + t * ldy + c), yv);
+  unpack8(*(const bf16x8*)(g + (t / tpf) * ldg + c), gv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = xv[e] + rb(gv[e] * yv[e]);
+  *(bf16x8*)(out + t * ldo + c) = pack8(o);
+}
+
 // ------------------------------------------------------------------ MSE loss + gradient
 // partial[block] = sum (pred - tgt)^2 over the block's elements; dpred = bf16(scale*(pred-tgt))
 __global__ __launch_bounds__(256) void mse_k(const bf16* __restrict__ pred, const bf16* __restrict__ tgt, long n8,
@@ -797,6 +817,18 @@ extern "C" int owlk_unpatchify(const void* tok, int C, int P, long BN, void* out
   hipLaunchKernelGGL(unpatchify_k, dim3((unsigned)BN), dim3(256), C * (P + 1) * sizeof(float), (hipStream_t)stream,
                      (const bf16*)tok, C, P, BN, (bf16*)out);
   return owlk::check_launch("unpatchify");
+}
+
+extern "C" int owlk_gate_resid(const void* x, long ldx, const void* y, long ldy, const void* g, long ldg, long tpf,
+                               long T, int d, void* out, long ldo, void* stream) {
+  OWLK_REQUIRE(d % 8 == 0 && T > 0 && tpf > 0 && T % tpf == 0, "gate_resid: bad sizes");
+  OWLK_REQUIRE((((uintptr_t)x | (uintptr_t)y | (uintptr_t)g | (uintptr_t)out) % 16 == 0) &&
+                   (ldx | ldy | ldg | ldo) % 8 == 0,
+               "gate_resid: rows must be 16-byte aligned");
+  const long work = T * (d / 8);
+  hipLaunchKernelGGL(gate_resid_k, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x, ldx, (const bf16*)y, ldy, (const bf16*)g, ldg, tpf, T, d, (bf16*)out, ldo);
+  return owlk::check_launch("gate_resid");
 }
 
 extern "C" int owlk_mse(const void* pred, const void* tgt, long n, float gscale, void* dpred, float* partial,

@@ -23,7 +23,7 @@ enum Epi : int {
   EPI_STORE = 0,       // C = alpha*acc (+ bf16(bias)) (+ beta*C_old)
   EPI_SILU = 1,        // aux = bf16(acc + bias); C = bf16(silu(aux))            (MLP fc1)
   EPI_GATE_RESID = 2,  // aux = y = bf16(acc + bias); C = bf16(resid + bf16(gate[m/tpf]*y))
-  EPI_DSILU = 3,       // C = bf16(bf16(acc) * silu'(aux))                        (MLP fc1 bwd)
+  EPI_DSILU = 3,       // C = bf16(bf16(acc) * silu'(aux)) (+ resid := bf16(silu(aux)))  (MLP fc1 bwd)
   EPI_AXPBY = 4,       // C = bf16(bf16(alpha*bf16(acc)) + bf16(beta*aux))        (Newton-Schulz)
   EPI_SCALE2 = 5,      // C = bf16(acc); aux = bf16(alpha*bf16(acc))   (NS: A = X X^T and c*A, muon.py:32-33)
 };
@@ -224,6 +224,12 @@ DEV void epi_chunk(const GemmP& p, long z, long gm, long gn, float (&v)[8]) {
       o[e] = rb(v[e]) * sg * (1.f + x[e] * (1.f - sg));
     }
     *(bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn) = pack8(o);
+    if (p.resid) {  // optional second output: the activation silu(aux) itself
+      float a[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = silu_f(x[e]);
+      *(bf16x8*)((bf16*)p.resid + z * p.sRes + gm * p.ldres + gn) = pack8(a);
+    }
   } else if (EPI == EPI_AXPBY) {
     float x[8], o[8];
     unpack8(*(const bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), x);
@@ -303,6 +309,12 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
       o[e] = rb(v[e]) * sg * (1.f + xx[e] * (1.f - sg));
     }
     st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(o));
+    if (p.resid) {  // optional second output: the activation silu(aux) itself
+      float a[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = silu_f(xx[e]);
+      st_nt((bf16x8*)((bf16*)p.resid + z * p.sRes + gm * p.ldres + gn), pack8(a));
+    }
     if (p.colsum) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += rb(o[e]);

@@ -50,6 +50,7 @@ _SIGS = {
     "owlk_unpatchify": [P, I, I, L, P, P],
     "owlk_mse": [P, P, L, F, P, P, I, P, P],
     "owlk_mse_grad": [P, P, L, F, P, P, P],
+    "owlk_gate_resid": [P, L, P, L, P, L, L, L, I, P, L, P],
     "owlk_colsum_ws_bytes": [L, L],
     "owlk_colsum": [P, I, L, L, L, P, P, L, P],
     "owlk_colsum_frames": [P, I, L, L, L, L, P, P, L, P],

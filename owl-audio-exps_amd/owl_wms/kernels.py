@@ -86,6 +86,7 @@ def gemm(A, B, *, a_trans=False, b_trans=False, out=None, out_f32=False, epi=EPI
     A: [M, K] (a_trans False) or [K, M] (a_trans True); B: [N, K] or [K, N] (b_trans True).
     A, B or out may instead be 3-D frame_rows views (frame-strided rows, the MMDiT joint layout).
     colsum: optional fp32 [N], += column sums of the stored bf16 C (fused into the DSILU epilogue).
+    With epi=EPI_DSILU a given resid is an OUTPUT: resid = bf16(silu(aux)).
     """
     if A.dim() == 3 or B.dim() == 3 or (out is not None and out.dim() == 3):
         assert colsum is None
@@ -236,6 +237,18 @@ def gate_bwd(dout, y, g, tpf, want_bias=True, dg_out=None):
     call("owlk_gate_bwd", ptr(dout), dout.stride(0), ptr(y), y.stride(0), ptr(g), g.stride(0), tpf, T, d, ptr(dy), d,
          ptr(dg), dg.stride(0), int(dg.dtype == BF16), ptr(dbf), d, stream())
     return dy, dg, dbf
+
+
+def gate_resid(x, y, g, tpf):
+    """bf16(x + bf16(g[t / tpf] * y)) for [T, d] row views (the GATE_RESID epilogue, recomputed)."""
+    T, d = x.shape
+    for t in (x, y, g):
+        assert t.dtype == BF16 and t.stride(1) == 1
+    assert y.shape == (T, d) and g.shape[1] == d and g.shape[0] * tpf == T
+    out = torch.empty(T, d, device=x.device, dtype=BF16)
+    call("owlk_gate_resid", ptr(x), x.stride(0), ptr(y), y.stride(0), ptr(g), g.stride(0), tpf, T, d, ptr(out), d,
+         stream())
+    return out
 
 
 def qk_rope_fwd(qkv, H, D, cos, sin, tab_off=0, tpos_div=0):

@@ -175,8 +175,10 @@ class DiTBlock(nn.Module):
         W, bvec = stacked_modulation_weights(self, mparams)
         H = cfg.n_heads
         rope = self.attn.rope
+        ck = getattr(self, "_checkpointed", False)
         geo = BlockGeometry(H, cfg.d_model // H, cfg.tokens_per_frame, block_mask, rope.cos, rope.sin, 0,
-                            keep_attn=id(self) if getattr(self, "_checkpointed", False) else None)
+                            keep_attn=id(self) if ck else None,
+                            lean=bool(getattr(cfg, "lean_activations", False)) and not ck)
         a, m = self.attn, self.mlp
         return DiTBlockFn.apply(x.to(torch.bfloat16).contiguous(), scond, W, bvec, geo, a.qkv.weight, a.qkv.bias,
                                 a.out.weight, a.out.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias,

@@ -297,10 +297,11 @@ class BlockGeometry:
     """Static per-forward data of a DiT block: heads, frame mask, RoPE tables; keep_attn = a key
     per block when the block runs under activation checkpointing (see _ATTN_KEEP)."""
 
-    def __init__(self, n_heads, head_dim, tpf, mask, cos, sin, tab_off=0, keep_attn=None):
+    def __init__(self, n_heads, head_dim, tpf, mask, cos, sin, tab_off=0, keep_attn=None, lean=False):
         self.H, self.D, self.tpf, self.mask = n_heads, head_dim, tpf, mask
         self.cos, self.sin, self.tab_off = cos, sin, tab_off
         self.keep_attn = keep_attn
+        self.lean = lean
 
 
 # A checkpointed block (dit_v4_5B: gradient_checkpointing, attn.py:186) runs its forward again
@@ -360,6 +361,12 @@ class DiTBlockFn(torch.autograd.Function):
         y2 = torch.empty(M, d, device=x.device, dtype=BF16)
         out = K.gemm(a, bf16_weight(w2), bias=b2, epi=K.EPI_GATE_RESID, aux=y2, gate=gg2, tpf=tpf, resid=x1)
 
+        if geo.lean:
+            # lean activations (memory-bound configs, e.g. dit_v4_5B with fewer checkpointed blocks):
+            # h1, h2 (adaln of kept inputs), the roped q / k, a = silu(a_pre) and x1 = x + g1 y1 are
+            # recomputed in the backward, bit for bit, from tensors kept anyway: 9 of 20 [T, d]
+            # bf16 units per block
+            h1 = qkr = h2 = a = x1 = None
         ctx.save_for_backward(xx, s2, wmod, mods, wqkv, wout, w1, w2, h1, r1, qkv, qkr, rq, o, lse, y1, x1, h2,
                               r2, a_pre, a, y2)
         ctx.geo, ctx.shape, ctx.sshape = geo, (B, T, d), s.shape
@@ -378,6 +385,8 @@ class DiTBlockFn(torch.autograd.Function):
         a1, gg1, a2, gg2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
         dx2 = dout.reshape(M, d).to(BF16).contiguous()
         dm = torch.empty_like(mods)  # d mods, bf16 as the modulation Linears' output gradient
+        if x1 is None:  # lean
+            x1 = K.gate_resid(xx, y1, gg1, tpf)
 
         prm = ctx.params  # (wqkv, bqkv, wout, bout, w1, b1, w2, b2, 4 x (w, b) mod) Parameters: gradient sinks
 
@@ -387,16 +396,24 @@ class DiTBlockFn(torch.autograd.Function):
         sink_b1 = grad_sink(prm[5])
         db1 = sink_b1 if sink_b1 is not None else torch.zeros(a_pre.shape[1], device=a_pre.device,
                                                               dtype=torch.float32)
-        dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=db1)  # + colsum
+        if a is None:  # lean: the dSiLU epilogue also emits a = silu(a_pre)
+            a = torch.empty_like(a_pre)
+            dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=db1, resid=a)
+        else:
+            dapre = K.gemm(dy2, bf16_weight(w2), b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=db1)  # + colsum
         if sink_b1 is not None:
             grad_done(prm[5])
             db1 = None
         dw2 = wgrad_into(prm[6], dy2, a)
+        del a
+        if h2 is None:
+            h2, _ = K.adaln_fwd(x1, a2[:, :d], a2[:, d:], tpf)
         dw1 = wgrad_into(prm[4], dapre, h2)
+        del h2
         dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
         del dapre
         dx1 = K.adaln_bwd_into(dh2, x1, r2, a2[:, :d], tpf, dm[:, 3 * d:5 * d], dres=dx2)
-        del dh2
+        del dh2, x1
 
         # ---- attention branch
         dy1, _, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf, dg_out=dm[:, 2 * d:3 * d])
@@ -404,6 +421,8 @@ class DiTBlockFn(torch.autograd.Function):
         do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
         dwout = wgrad_into(prm[2], dy1, o)
         del dy1
+        if qkr is None:
+            qkr, _ = K.qk_rope_fwd(qkv, H, D, geo.cos, geo.sin, geo.tab_off, T)
         dqkv = torch.empty(M, 3 * d, device=xx.device, dtype=BF16)
         dqkr = torch.empty(M, 2 * d, device=xx.device, dtype=BF16)
         q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
@@ -420,7 +439,11 @@ class DiTBlockFn(torch.autograd.Function):
         if sink_bqkv is not None:
             grad_done(prm[1])
             dbqkv = None
+        del qkr, q3, k3
+        if h1 is None:
+            h1, _ = K.adaln_fwd(xx, a1[:, :d], a1[:, d:], tpf)
         dwqkv = wgrad_into(prm[0], dqkv, h1)
+        del h1
         dh1 = K.gemm(dqkv, bf16_weight(wqkv), b_trans=True)
         del dqkv
         dx = K.adaln_bwd_into(dh1, xx, r1, a1[:, :d], tpf, dm[:, :2 * d], dres=dx1)

@@ -363,15 +363,17 @@ def test_checkpointed_blocks_reuse_attention():
     """gradient_checkpointing (dit_v4_5B): the re-run of each block inside backward takes the
     attention output kept from the first pass, so one attention forward runs per layer per step;
     loss and every gradient equal the non-checkpointed step (the re-run is bit-exact; fp32-atomic
-    bias-gradient sums aside, hence a 1e-6 bound)."""
+    bias-gradient sums aside, hence a 1e-6 bound).  lean_activations (h1, h2, roped q / k and
+    silu(a_pre) recomputed in the backward of non-checkpointed blocks) gives the same step too."""
     from owl_wms import _lib
     from owl_wms.configs import model_config
     from owl_wms.models.flow import InjectedNoise
     from owl_wms.models.gamerft import GameRFT
     p = "gamerft.bf16."
     grads, losses, nfwd = [], [], []
-    for ckpt, n_ck in ((False, None), (True, None), (True, 1)):  # n_ck: checkpoint_layers (first n only)
-        kw = dict(TINY, gradient_checkpointing=ckpt)
+    runs = ((False, None, False), (True, None, False), (True, 1, False), (False, None, True), (True, 1, True))
+    for ckpt, n_ck, lean in runs:  # n_ck: checkpoint_layers (first n only)
+        kw = dict(TINY, gradient_checkpointing=ckpt, lean_activations=lean)
         if n_ck is not None:
             kw["checkpoint_layers"] = n_ck
         m = det_init_(GameRFT(model_config(**kw)), base_seed=1000).cuda().train()
@@ -385,8 +387,8 @@ def test_checkpointed_blocks_reuse_attention():
         nfwd.append(sum(n for k, (n, _, _) in prof.items() if k.startswith("attn_fwd")))
         losses.append(loss.item())
         grads.append({k: q.grad.detach().clone() for k, q in m.named_parameters() if q.grad is not None})
-    assert nfwd == [TINY["n_layers"]] * 3
-    for j in (1, 2):
+    assert nfwd == [TINY["n_layers"]] * len(runs)
+    for j in range(1, len(runs)):
         assert losses[0] == losses[j]
         assert grads[0].keys() == grads[j].keys()
         for k in grads[0]:
