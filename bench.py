@@ -177,23 +177,31 @@ def microsteps(args):
     from owl_wms.configs import Config
     from owl_wms.data import synthetic_video_batch
     from owl_wms.models import get_model_cls
+    from owl_wms.utils.grad_reducer import GradReducer
     cfg = Config.from_yaml(os.path.join(REPO, args.config))
     mc = cfg.model
     if args.frames:
         mc.n_frames = args.frames
+    if args.ckpt_layers is not None:
+        mc.checkpoint_layers = args.ckpt_layers
+    if args.lean is not None:
+        mc.lean_activations = bool(args.lean)
     torch.manual_seed(0)
     log("[microsteps] building the model")
     model = get_model_cls(mc.model_id)(mc).cuda().train()
+    # gradients accumulate into GradReducer bucket views as in the timed step (direct dW / db writes)
+    red = GradReducer(model.parameters(), world_size=1)
     b = [t.cuda() for t in synthetic_video_batch(mc, 1, seed=1234, n_docs=args.docs)]
     for i in range(args.microsteps):
         log(f"[microsteps] micro-step {i}")
+        red.begin(False)
         if mc.model_id == "game_rft_audio":
             au = torch.randn(1, mc.n_frames, mc.audio_channels, device="cuda").to(torch.bfloat16)
             loss = model(b[0] / cfg.train.vae_scale, au, b[1], b[2])[0]
         else:
             loss = model(b[0] / cfg.train.vae_scale, b[1], b[2], b[3])
         loss.backward()
-        model.zero_grad(set_to_none=True)
+        red.finish()
     torch.cuda.synchronize()
     log("[microsteps] done")
 

@@ -9,7 +9,7 @@ import torch  # noqa: E402
 from owl_wms import kernels as K  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "fwd"
-H, D, tpf, nf = 24, 64, 64, int(os.environ.get("FRAMES", "512"))
+H, D, tpf, nf = int(os.environ.get("HEADS", "24")), int(os.environ.get("DIM", "64")), 64, int(os.environ.get("FRAMES", "512"))
 L = nf * tpf
 torch.manual_seed(0)
 qkv = torch.randn(1, L, 3 * H * D, device="cuda", dtype=torch.bfloat16)
