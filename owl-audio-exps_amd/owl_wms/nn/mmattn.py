@@ -26,7 +26,7 @@ import torch
 from torch import nn
 
 from .. import kernels as K
-from .fused import bf16_weight, cond_silu, linear
+from .fused import bf16_weight, cond_silu, grad_done, grad_sink, linear
 from .mlp import MLP
 from .rope import get_rope_cls
 
@@ -150,6 +150,7 @@ class MMDiTBlockFn(torch.autograd.Function):
         lane.join()
         ctx.save_for_backward(qkvj, qkr, rq, o, lse, *saved[0], *saved[1], *w)
         ctx.geo, ctx.dims = geo, (B, T0, x1.shape[1], d, T, nf)
+        ctx.params = w  # the Parameters themselves: their GradReducer bucket views are the gradient sinks
         return outs[0].view(B, T0, d), outs[1].view(B, x1.shape[1], d)
 
     @staticmethod
@@ -162,6 +163,31 @@ class MMDiTBlockFn(torch.autograd.Function):
         H, D, n0, n1 = geo.H, geo.D, geo.n0, geo.n1
         ns = (n0, n1)
         dW = [None] * 16
+        prm = ctx.params
+        done = []  # parameters whose bucket view is complete, reported to the reducer on the main stream
+
+        def wgrad(i, dy, x):  # dW_i = dy^T x straight into the bucket view (beta 1) or returned
+            sink = grad_sink(prm[i])
+            if sink is None:
+                dW[i] = K.gemm_wgrad(dy, x)
+            else:
+                K.gemm(dy, x, a_trans=True, b_trans=True, out=sink, out_f32=True, beta=1.0)
+                done.append(prm[i])
+
+        def bgrad(i, rows):  # db_i = column sums of rows (bf16 rows or fp32 per-frame partials)
+            sink = grad_sink(prm[i])
+            if sink is None:
+                dW[i] = K.colsum(rows)
+            else:
+                K.colsum(rows, out=sink)
+                done.append(prm[i])
+
+        def report():  # after a lane join: every write above is ordered before the main stream's next work
+            for q in done:
+                grad_done(q)
+            done.clear()
+
+        dcs = [torch.empty(nf, 6 * d, device=dout0.device, dtype=BF16) for _ in range(2)]  # d mods, bf16
         douts = (dout0.reshape(-1, d).to(BF16).contiguous(), dout1.reshape(-1, d).to(BF16).contiguous())
         inplace = _in_place_ok(d, n0, n1)
         lane = _AudioLane(o.device, inplace)
@@ -171,31 +197,39 @@ class MMDiTBlockFn(torch.autograd.Function):
             do_dst = _joint_views(do, n0, n1, d)
         else:
             os_ = K.frame_split(o.view(B * T, d), n0, n1)
-        dos, dx1s, dmods = [None, None], [None, None], [[None] * 4, [None] * 4]
+        dos, dx1s = [None, None], [None, None]
         wts = [[bf16_weight(w[10 + 4 * s]), bf16_weight(w[8 + 4 * s]), bf16_weight(w[4 + 2 * s])] for s in range(2)]
         lane.fork()
         for s in (1, 0):
             with lane.on(s):
                 xs, ms, h1, r1, y1, x1s, h2, r2, a_pre, a, y2 = st[s]
+                dm = dcs[s]
                 # ---- MLP
-                dy2, dg2, dbf2 = K.gate_bwd(douts[s], y2, ms[:, 5 * d:], ns[s])
-                dW[11 + 4 * s] = dbf2.sum(0)
-                dW[9 + 4 * s] = torch.zeros(a_pre.shape[1], device=a_pre.device, dtype=torch.float32)
-                dapre = K.gemm(dy2, wts[s][0], b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=dW[9 + 4 * s])
-                dW[10 + 4 * s] = K.gemm_wgrad(dy2, a)
-                dW[8 + 4 * s] = K.gemm_wgrad(dapre, h2)
+                dy2, _, dbf2 = K.gate_bwd(douts[s], y2, ms[:, 5 * d:], ns[s], dg_out=dm[:, 5 * d:])
+                bgrad(11 + 4 * s, dbf2)
+                i_b1 = 9 + 4 * s
+                sink_b1 = grad_sink(prm[i_b1])
+                cs = sink_b1 if sink_b1 is not None else torch.zeros(a_pre.shape[1], device=a_pre.device,
+                                                                     dtype=torch.float32)
+                dapre = K.gemm(dy2, wts[s][0], b_trans=True, epi=K.EPI_DSILU, aux=a_pre, colsum=cs)
+                if sink_b1 is not None:
+                    done.append(prm[i_b1])
+                else:
+                    dW[i_b1] = cs
+                wgrad(10 + 4 * s, dy2, a)
+                wgrad(8 + 4 * s, dapre, h2)
                 dh2 = K.gemm(dapre, wts[s][1], b_trans=True)
                 del dapre, dy2
-                dx1, dmod2 = K.adaln_bwd(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dres=douts[s])
+                dx1 = K.adaln_bwd_into(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dm[:, 3 * d:5 * d], dres=douts[s])
                 # ---- attention output projection
-                dy1, dg1, dbf1 = K.gate_bwd(dx1, y1, ms[:, 2 * d:3 * d], ns[s])
-                dW[5 + 2 * s] = dbf1.sum(0)
+                dy1, _, dbf1 = K.gate_bwd(dx1, y1, ms[:, 2 * d:3 * d], ns[s], dg_out=dm[:, 2 * d:3 * d])
+                bgrad(5 + 2 * s, dbf1)
                 dos[s] = K.gemm(dy1, wts[s][2], b_trans=True, out=do_dst[s] if inplace else None)
-                dW[4 + 2 * s] = K.gemm_wgrad(dy1, os_[s])
+                wgrad(4 + 2 * s, dy1, os_[s])
                 dx1s[s] = dx1
-                dmods[s][1], dmods[s][2], dmods[s][3] = dg1, dmod2, dg2
-        lane.mark([dW[i] for i in (6, 7, 12, 13, 14, 15)] + [dx1s[1]] + dmods[1][1:] + [dos[1]])  # audio's
+        lane.mark([dW[i] for i in (6, 7, 12, 13, 14, 15)] + [dx1s[1]] + [dos[1]])  # audio's
         lane.join()
+        report()
         del os_
         if not inplace:
             do = K.frame_interleave(dos[0], dos[1], n0, n1)
@@ -211,22 +245,21 @@ class MMDiTBlockFn(torch.autograd.Function):
         del dqkr
         # the per-modality qkv gradients: views of the joint rows (in place) or split copies
         dqkv = _joint_views(dqkvj, n0, n1, 3 * d) if inplace else K.frame_split(dqkvj, n0, n1)
-        dxs, dcs = [None, None], [None, None]
+        dxs = [None, None]
         wq = [bf16_weight(w[2 * s]) for s in range(2)]
         lane.fork()
         for s in (1, 0):
             with lane.on(s):
                 xs, ms, h1, r1 = st[s][:4]
-                dW[1 + 2 * s] = K.colsum(dqkv[s])
-                dW[2 * s] = K.gemm_wgrad(dqkv[s], h1)
+                bgrad(1 + 2 * s, dqkv[s])
+                wgrad(2 * s, dqkv[s], h1)
                 dh1 = K.gemm(dqkv[s], wq[s], b_trans=True)
-                dx, dmod1 = K.adaln_bwd(dh1, xs, r1, ms[:, :d], ns[s], dres=dx1s[s])
-                dxs[s] = dx
-                _, dg1, dmod2, dg2 = dmods[s]
-                dcs[s] = torch.cat([dmod1, dg1, dmod2, dg2], dim=1).view(B, nf // B, 6 * d)
+                dxs[s] = K.adaln_bwd_into(dh1, xs, r1, ms[:, :d], ns[s], dcs[s][:, :2 * d], dres=dx1s[s])
         lane.mark([dW[3], dW[2], dxs[1], dcs[1]])
         lane.join()
-        return (dxs[0].view(B, T0, d), dxs[1].view(B, T1, d), dcs[0], dcs[1], None, *dW)
+        report()
+        return (dxs[0].view(B, T0, d), dxs[1].view(B, T1, d), dcs[0].view(B, nf // B, 6 * d),
+                dcs[1].view(B, nf // B, 6 * d), None, *dW)
 
 
 class MMAttn(nn.Module):
