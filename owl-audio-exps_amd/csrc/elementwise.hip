@@ -91,9 +91,35 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
       for (int e = 0; e < 8; ++e) t1[i][e] = rb(1.f + a[e]);
     }
   }
+  // the wave's next row (dy, x, dres, rstd) is loaded while the current one is reduced and stored:
+  // two rows of 16-B loads in flight per lane instead of one
+  bf16x8 ndy[MAXC], nx[MAXC], nres[MAXC];
+  float nr = 0.f;
+  auto load = [&](long t) {
+    const long row = f * tpf + t;
+    nr = rstd[row];
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        ndy[i] = *(const bf16x8*)(dy + row * lddy + c * 8);
+        nx[i] = *(const bf16x8*)(x + row * ldx + c * 8);
+        if (dres) nres[i] = *(const bf16x8*)(dres + row * ldres + c * 8);
+      }
+    }
+  };
+  if (w < tpf) load(w);
   for (long t = w; t < tpf; t += 4) {
     const long row = f * tpf + t;
-    const float r = rstd[row];
+    const float r = nr;
+    bf16x8 cdy[MAXC], cx[MAXC], cres[MAXC];
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      cdy[i] = ndy[i];
+      cx[i] = nx[i];
+      cres[i] = nres[i];
+    }
+    if (t + 4 < tpf) load(t + 4);
     float g[MAXC][8], xh[MAXC][8];
     float dot = 0.f;
 #pragma unroll
@@ -101,8 +127,8 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
       const int c = lane + 64 * i;
       if (c < nch) {
         float dv[8], xv[8];
-        unpack8(*(const bf16x8*)(dy + row * lddy + c * 8), dv);
-        unpack8(*(const bf16x8*)(x + row * ldx + c * 8), xv);
+        unpack8(cdy[i], dv);
+        unpack8(cx[i], xv);
         if (ypre) {  // FinalLayer: dy arrives as d silu(y); silu backward in bf16 like autocast
           float yp[8];
           unpack8(*(const bf16x8*)(ypre + row * lddy + c * 8), yp);
@@ -129,7 +155,7 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
       const int c = lane + 64 * i;
       if (c < nch) {
         float o[8], rs[8];
-        if (dres) unpack8(*(const bf16x8*)(dres + row * ldres + c * 8), rs);
+        if (dres) unpack8(cres[i], rs);
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = r * (g[i][e] - xh[i][e] * dot) + (dres ? rs[e] : 0.f);
         *(bf16x8*)(dx + row * lddx + c * 8) = pack8(o);
@@ -187,15 +213,36 @@ __global__ __launch_bounds__(256) void gate_bwd_k(const bf16* __restrict__ dout,
     for (int e = 0; e < 8; ++e) pg[i][e] = pb[i][e] = 0.f;
     if (c < nch) unpack8(*(const bf16x8*)(g + f * ldg + c * 8), gv[i]);
   }
-  for (long t = w; t < tpf; t += 4) {
+  // the wave's next row is loaded while the current one is processed (two rows in flight)
+  bf16x8 nd[MAXC], ny[MAXC];
+  auto load = [&](long t) {
     const long row = f * tpf + t;
 #pragma unroll
     for (int i = 0; i < MAXC; ++i) {
       const int c = lane + 64 * i;
       if (c < nch) {
+        nd[i] = *(const bf16x8*)(dout + row * ldo + c * 8);
+        ny[i] = *(const bf16x8*)(y + row * ldy + c * 8);
+      }
+    }
+  };
+  if (w < tpf) load(w);
+  for (long t = w; t < tpf; t += 4) {
+    const long row = f * tpf + t;
+    bf16x8 cd[MAXC], cy[MAXC];
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      cd[i] = nd[i];
+      cy[i] = ny[i];
+    }
+    if (t + 4 < tpf) load(t + 4);
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
         float dv[8], yv[8], o[8];
-        unpack8(*(const bf16x8*)(dout + row * ldo + c * 8), dv);
-        unpack8(*(const bf16x8*)(y + row * ldy + c * 8), yv);
+        unpack8(cd[i], dv);
+        unpack8(cy[i], yv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           pg[i][e] += dv[e] * yv[e];
