@@ -14,6 +14,10 @@
 #include "attn_common.hpp"
 
 
+#ifndef OWLK_DKDV_ORDER
+#define OWLK_DKDV_ORDER 0
+#endif
+
 namespace {
 
 constexpr int TB = 128;              // rows owned by a workgroup (4 waves x 32)
@@ -366,7 +370,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
 }
 
 // ======================================================================== dK, dV on 16x16x32 MFMAs
-// The same workgroup, ring and tile classes as attn_bwd_dkdv_k, with every product on
+// The same workgroup, ring and tile classes as attn_bwd_dkdv_k (D 64), with every product on
 // v_mfma_f32_16x16x32_bf16: the chip holds a higher clock on that shape than on 32x32x16 at the same
 // cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7).  Per wave 32 keys as two 16-key
 // column tiles (lane column c = lane & 15, k-group g = lane >> 4); per 32-query block two 16-row
@@ -375,17 +379,13 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_k(BwdP p) 
 // permuted: slot j of group g is query 4 g + j (j < 4) or 16 + 4 g + (j - 4); the A operands dO^T
 // and Q^T are read in that order by two ds_read_b64_tr_b16 per fragment (rows 4 g .. 4 g + 3 and
 // 16 + 4 g .. + 3 of the tile, columns 16 ds + 4 (c & 3) .. + 3).
-// D 128 (dit_v4_5B): the same body over D / 64 column sub-tiles with QT = 1 and a two-slot ring
-// (65 KiB), so two workgroups share a CU (two waves per SIMD) where the 32x32x16 kernel ran one.
-template <int D, int QT_>
-__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p) {
-  using C = Cfg<D>;
+template <int QT_>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(BwdP p) {
+  constexpr int D = 64;
   using G = DkdvCfg<D, QT_>;
   constexpr int QT = G::QT, TLQ = G::TLQ, NBUF = G::NBUF;
-  constexpr int NSUB = C::NSUB, KS = D / 32, DS = D / 16;
-  constexpr int BUF = 2 * QT * NSUB * SUB + 2 * TLQ * 4;  // Q [QT][NSUB] | dO [QT][NSUB] | lse2 | delta
+  constexpr int BUF = 2 * QT * SUB + 2 * TLQ * 4;  // Q [QT] | dO [QT] | lse2 | delta
   constexpr int LSEW = TLQ / 64;
-  static_assert(D == 128 || NBUF * BUF + 16 <= 80 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF + 16];
   int& red_hi = *(int*)(smem + NBUF * BUF);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -427,12 +427,12 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
   // this lane's two keys (column c of the wave's two 16-key tiles) as B operands, k' = bf16(-c k),
   // v' = -v (row constants in the accumulators, as attn_bwd_dkdv_k)
   long my_k[2];
-  bf16x8 kf[2][KS], vf[2][KS];  // [key tile][k step of 32 d]
+  bf16x8 kf[2][2], vf[2][2];  // [key tile][k step of 32 d]
 #pragma unroll
   for (int t2 = 0; t2 < 2; ++t2) {
     my_k[t2] = kw0 + 16 * t2 + c;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int ks = 0; ks < 2; ++ks) {
       bf16x8 kv = my_k[t2] < p.Lkv ? *(const bf16x8*)(K + my_k[t2] * p.ldk + 32 * ks + 8 * g) : bf16x8{};
       bf16x8 vv = my_k[t2] < p.Lkv ? *(const bf16x8*)(V + my_k[t2] * p.ldv + 32 * ks + 8 * g) : bf16x8{};
       float f[8], h8[8];
@@ -455,9 +455,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
 
-  f32x4 dk[DS][2], dv[DS][2];  // [16-column d tile][key tile]
+  f32x4 dk[4][2], dv[4][2];  // [16-column d tile][key tile]
 #pragma unroll
-  for (int ds = 0; ds < DS; ++ds)
+  for (int ds = 0; ds < 4; ++ds)
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) dk[ds][t2] = dv[ds][t2] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -466,17 +466,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
 #pragma unroll
     for (int sq = 0; sq < QT; ++sq) {
       const long r = q0 + 64 * sq;
-      char* bq = buf + sq * NSUB * SUB;
-      char* bd = buf + (QT + sq) * NSUB * SUB;
-#pragma unroll
-      for (int sb = 0; sb < NSUB; ++sb) {
-        if (r + TL <= p.Lq) {
-          tile_glds_fast(bq + sb * SUB, Q + r * p.ldq + 64 * sb, go_q, w);
-          tile_glds_fast(bd + sb * SUB, dO + r * p.ldo + 64 * sb, go_d, w);
-        } else {
-          tile_glds<SW_DUAL>(bq + sb * SUB, Q + 64 * sb, p.ldq, r, p.Lq, w, lane);
-          tile_glds<SW_DUAL>(bd + sb * SUB, dO + 64 * sb, p.ldo, r, p.Lq, w, lane);
-        }
+      char* bq = buf + sq * SUB;
+      char* bd = buf + (QT + sq) * SUB;
+      if (r + TL <= p.Lq) {
+        tile_glds_fast(bq, Q + r * p.ldq, go_q, w);
+        tile_glds_fast(bd, dO + r * p.ldo, go_d, w);
+      } else {
+        tile_glds<SW_DUAL>(bq, Q, p.ldq, r, p.Lq, w, lane);
+        tile_glds<SW_DUAL>(bd, dO, p.ldo, r, p.Lq, w, lane);
       }
     }
     if (w < 2 * LSEW) {
@@ -485,10 +482,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
       const long n = p.Lq - r;
       const int i = r + 64 <= p.Lq ? lane : (lane < n ? lane : (n > 0 ? (int)n - 1 : 0));
       const long src = r + i < p.Lq ? r + i : p.Lq - 1;
-      glds_f32(buf + 2 * QT * NSUB * SUB + ((w & 1) * TLQ + 64 * part) * 4, ((w & 1) ? DLT : LSE) + src);
+      glds_f32(buf + 2 * QT * SUB + ((w & 1) * TLQ + 64 * part) * 4, ((w & 1) ? DLT : LSE) + src);
     }
   };
-  constexpr int OPS = 4 * QT * NSUB;
+  constexpr int OPS = 4 * QT;
   auto wait_oldest = [&](int younger) {
     if (younger <= 0)
       vmcnt<0>();
@@ -507,7 +504,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
     const long q0 = qbeg + (long)t * TLQ;
     if (t + NBUF - 1 < ntiles) issue(smem + ((t + NBUF - 1) % NBUF) * BUF, q0 + (long)(NBUF - 1) * TLQ);
     const char* tb = smem + (t % NBUF) * BUF;
-    const float* l2 = (const float*)(tb + 2 * QT * NSUB * SUB);
+    const float* l2 = (const float*)(tb + 2 * QT * SUB);
     const float* dlt = l2 + TLQ;
 
     int kind = TILE_FULL;
@@ -523,8 +520,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
       const bool masked = kind == TILE_PARTIAL;
 #pragma unroll
       for (int sq = 0; sq < QT; ++sq) {
-        const char* lq = tb + sq * NSUB * SUB;
-        const char* ld = tb + (QT + sq) * NSUB * SUB;
+        const char* lq = tb + sq * SUB;
+        const char* ld = tb + (QT + sq) * SUB;
         unsigned long long bh[2] = {0ull, 0ull};
         if (masked) {
 #pragma unroll
@@ -542,12 +539,48 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
             st[qs][0] = st[qs][1] = L;
             dp[qs][0] = dp[qs][1] = Dl;
           }
+#if OWLK_DKDV_ORDER
+          // the S chain first, then the dP chain: the exp2 of P issues in the gaps of the dP MFMAs
 #pragma unroll
-          for (int ks = 0; ks < KS; ++ks)
+          for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int qs = 0; qs < 2; ++qs) {
-              const bf16x8 aq = frag_row16(lq + (ks >> 1) * SUB, 32 * qb + 16 * qs, ks & 1, lane);
-              const bf16x8 ad = frag_row16(ld + (ks >> 1) * SUB, 32 * qb + 16 * qs, ks & 1, lane);
+              const bf16x8 aq = frag_row16(lq, 32 * qb + 16 * qs, ks, lane);
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2)
+                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kf[t2][ks], st[qs][t2], 0, 0, 0);
+            }
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+              const bf16x8 ad = frag_row16(ld, 32 * qb + 16 * qs, ks, lane);
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2)
+                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vf[t2][ks], dp[qs][t2], 0, 0, 0);
+            }
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
+#if OWLK_DKDV_ORDER == 1
+          // pin the order: the 8 S MFMAs, then each dP MFMA followed by two exp2 (VALU)
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+#endif
+#else
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+              const bf16x8 aq = frag_row16(lq, 32 * qb + 16 * qs, ks, lane);
+              const bf16x8 ad = frag_row16(ld, 32 * qb + 16 * qs, ks, lane);
 #pragma unroll
               for (int t2 = 0; t2 < 2; ++t2) {
                 st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kf[t2][ks], st[qs][t2], 0, 0, 0);
@@ -560,6 +593,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
               for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
+#endif
           if (masked) {
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2) {
@@ -573,6 +607,42 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
             }
           }
           bf16x8 pf[2], sf[2];
+#if OWLK_DKDV_ORDER
+          // P packed first: the dV MFMAs run while dS = P o (dP - delta) is formed and packed
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) pf[t2] = pack_perm(st[0][t2], st[1][t2]);
+#pragma unroll
+          for (int ds = 0; ds < 4; ++ds) {
+            const bf16x8 ado = frag_tr16(ld, 32 * qb, ds, lane);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+              dv[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pf[t2], dv[ds][t2], 0, 0, 0);
+          }
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) {
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) dp[qs][t2][r] *= st[qs][t2][r];
+            sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
+          }
+#if OWLK_DKDV_ORDER == 1
+          // pin: P pack (8 cvt), then each dV MFMA followed by its share of the dS VALU (16 mul + 8 cvt)
+          __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 1);
+          }
+#endif
+#pragma unroll
+          for (int ds = 0; ds < 4; ++ds) {
+            const bf16x8 aqt = frag_tr16(lq, 32 * qb, ds, lane);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+              dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
+          }
+#else
 #pragma unroll
           for (int t2 = 0; t2 < 2; ++t2) {
 #pragma unroll
@@ -583,15 +653,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
             sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
           }
 #pragma unroll
-          for (int ds = 0; ds < DS; ++ds) {
-            const bf16x8 ado = frag_tr16(ld + (ds >> 2) * SUB, 32 * qb, ds & 3, lane);
-            const bf16x8 aqt = frag_tr16(lq + (ds >> 2) * SUB, 32 * qb, ds & 3, lane);
+          for (int ds = 0; ds < 4; ++ds) {
+            const bf16x8 ado = frag_tr16(ld, 32 * qb, ds, lane);
+            const bf16x8 aqt = frag_tr16(lq, 32 * qb, ds, lane);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2) {
               dv[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pf[t2], dv[ds][t2], 0, 0, 0);
               dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
             }
           }
+#endif
         }
       }
     }
@@ -606,7 +677,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
     bf16* pk = p.dk + b * p.sdkb + my_k[t2] * p.lddk + head * D + 4 * g;
     bf16* pv = p.dv + b * p.sdvb + my_k[t2] * p.lddv + head * D + 4 * g;
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
+    for (int ds = 0; ds < 4; ++ds) {
       bf16x4 a4, b4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -615,309 +686,6 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv16_k(BwdP p
       }
       *(bf16x4*)(pk + 16 * ds) = a4;
       *(bf16x4*)(pv + 16 * ds) = b4;
-    }
-  }
-}
-
-// ======================================================================== dK, dV by wave pairs (D 128)
-// D 128 does not fit attn_bwd_dkdv16_k's two-waves-per-SIMD register budget (dK^T, dV^T and the K / V
-// operands of 32 keys are 192 registers), and the 32x32x16 kernel at one wave per SIMD leaves the
-// MFMA pipe idle while its one wave waits.  Here a 512-thread workgroup (128 keys, one per CU, two
-// waves per SIMD) splits each 32-key group's products between two waves of one pair:
-//   wave a (w < 4):  S = Q K'^T (+lse2), P = exp2(-S), dV^T += dO^T P  -> hands P (fp32) to wave b
-//   wave b (w >= 4): dP' = dO V'^T (+delta), dS' = P o dP',  dK^T += Q^T dS'
-// so each wave holds one operand set (K' or V') and one accumulator set (dV or dK).  Wave b runs its
-// dP chain one 32-query block ahead of the P it consumes, so the MFMAs of dP(i + 1) cover wave a's
-// softmax of block i.  P crosses LDS once per 32 x 32 block (4 KiB, lane-linear, conflict-free)
-// through an NPS-slot mailbox per pair with produced / consumed counters in LDS: a waits for the
-// slot it reuses to be consumed, b for the block it reads to be produced.  Both waves see the same
-// tile kinds (same keys), so they step through the same blocks, and neither waits on the other at
-// a barrier the other has not reached (a's wait is on a block of the current tile, which b has
-// consumed before it reaches the tile barrier).  Spins are bounded.  The results are those of
-// attn_bwd_dkdv16_k: the same fp32 P, dS and bf16 roundings.
-template <int D, int QT>
-struct PairCfg {
-  static constexpr int NBUF = QT == 2 ? 2 : 3, NPS = QT == 2 ? 1 : 2;
-};
-template <int D, int QT>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_pair_k(BwdP p) {
-  constexpr int TLQ = TL * QT, NBUF = PairCfg<D, QT>::NBUF, NPS = PairCfg<D, QT>::NPS;
-  constexpr int NSUB = D / 64, KS = D / 32, DS = D / 16, NB = 2 * QT;
-  constexpr int XB = QT * NSUB * SUB;                 // one operand (Q or dO) of a ring slot
-  constexpr int BUF = 2 * XB + 2 * TLQ * 4;           // Q [QT][NSUB] | dO [QT][NSUB] | lse2 | delta
-  constexpr int PSLOT = 64 * 16 * 4;                  // one 32 x 32 fp32 block, 16 floats per lane
-  constexpr int MB = NBUF * BUF;                      // mailbox base
-  constexpr int FL = MB + 4 * NPS * PSLOT;            // counters: [pair] produced, [4 + pair] consumed, [8] red_hi
-  static_assert(FL + 64 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[FL + 64];
-  int* cnt = (int*)(smem + FL);
-  int& red_hi = cnt[8];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int pr = w & 3;
-  const bool is_a = w < 4;
-  const int c = lane & 15, g = lane >> 4;
-  const BlockIds bid = xcd_block_ids();
-  const long b = bid.z;
-  const int head = bid.y;
-  const long k0 = (long)bid.x * TB;
-  const long kw0 = k0 + 32 * pr;
-  const MaskP& m = p.m;
-
-  const bf16* Q = p.q + b * p.sqb + head * D;
-  const bf16* K = p.k + b * p.skb + head * D;
-  const bf16* V = p.v + b * p.svb + head * D;
-  const bf16* dO = p.dout + b * p.sob + head * D;
-  const float* LSE = p.lse + (b * p.H + head) * p.Lq;
-  const float* DLT = p.delta + (b * p.H + head) * p.Lq;
-
-  if (threadIdx.x < 8) cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const long klast = (k0 + TB < p.Lkv ? k0 + TB : p.Lkv) - 1;
-  const int fk_lo = frame_of(m, k0), fk_hi = frame_of(m, klast);
-  int fq_end;
-  if (m.q_hi) {
-    if (threadIdx.x == 0) red_hi = -1;
-    __syncthreads();
-    int mx = -1;
-    for (int f = fk_lo + threadIdx.x; f <= fk_hi; f += 512) mx = max(mx, m.q_hi[b * m.fstride + f]);
-    atomicMax(&red_hi, mx);
-    __syncthreads();
-    fq_end = red_hi;
-  } else {
-    fq_end = m.window > 0 ? min(m.n_frames - 1, fk_hi + m.window - 1) : m.n_frames - 1;
-  }
-  const int fq_start = m.causal ? fk_lo : (m.window > 0 ? max(0, fk_lo - m.window + 1) : 0);
-  long qbeg = ((long)fq_start * m.tpf / TL) * TL;
-  long qend = ((long)fq_end + 1) * m.tpf;
-  if (qend > p.Lq) qend = p.Lq;
-  const int ntiles = qend > qbeg ? (int)((qend - qbeg + TLQ - 1) / TLQ) : 0;
-
-  // this lane's two keys as B operands: wave a k' = bf16(-c k), wave b v' = -v
-  long my_k[2];
-  bf16x8 bo[2][KS];  // [key tile][k step of 32 d]
-  const bf16* KV = is_a ? K : V;
-  const long ldkv = is_a ? p.ldk : p.ldv;
-  const float mul = is_a ? -p.scale_log2 : -1.f;
-#pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2) {
-    my_k[t2] = kw0 + 16 * t2 + c;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 kv = my_k[t2] < p.Lkv ? *(const bf16x8*)(KV + my_k[t2] * ldkv + 32 * ks + 8 * g) : bf16x8{};
-      float f[8];
-      unpack8(kv, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= mul;
-      bo[t2][ks] = pack8(f);
-    }
-  }
-  const bool wave_live = kw0 < p.Lkv;
-  const long wklast = (kw0 + 31 < p.Lkv ? kw0 + 31 : p.Lkv - 1);
-  const int wfk0 = frame_of(m, kw0), wfk1 = frame_of(m, wklast);
-  TileRange full = full_range_q(m, b, wfk0, wfk1, qbeg, p.Lq, TLQ);
-  if (!wave_live || kw0 + 32 > p.Lkv) full = TileRange{1, 0};
-  full.lo = __builtin_amdgcn_readfirstlane(full.lo);
-  full.hi = __builtin_amdgcn_readfirstlane(full.hi);
-
-  f32x4 acc[DS][2];  // wave a: dV^T, wave b: dK^T  [16-column d tile][key tile]
-#pragma unroll
-  for (int ds = 0; ds < DS; ++ds)
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) acc[ds][t2] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // LDS-DMA: waves 0-3 move the Q sub-tiles (16 rows of each 64-row part), waves 4-7 the dO
-  // sub-tiles; waves 0 / 4 (and 1 / 5 at QT 2) the 64-float parts of the lse2 / delta rows
-  const GldsOff go = glds_offsets<SW_DUAL>(is_a ? p.ldq : p.ldo, pr, lane);
-  const bf16* X = is_a ? Q : dO;
-  const long ldx = is_a ? p.ldq : p.ldo;
-  const bool row_wave = pr < QT;
-  auto issue = [&](char* buf, long q0) {
-    char* bx = buf + (is_a ? 0 : XB);
-#pragma unroll
-    for (int sq = 0; sq < QT; ++sq) {
-      const long r = q0 + 64 * sq;
-#pragma unroll
-      for (int sb = 0; sb < NSUB; ++sb) {
-        char* dst = bx + (sq * NSUB + sb) * SUB;
-        if (r + TL <= p.Lq)
-          tile_glds_fast(dst, X + r * ldx + 64 * sb, go, pr);
-        else
-          tile_glds<SW_DUAL>(dst, X + 64 * sb, ldx, r, p.Lq, pr, lane);
-      }
-    }
-    if (row_wave) {
-      const long r = q0 + 64 * pr;
-      const long n = p.Lq - r;
-      const int i = r + 64 <= p.Lq ? lane : (lane < n ? lane : (n > 0 ? (int)n - 1 : 0));
-      const long src = r + i < p.Lq ? r + i : p.Lq - 1;
-      glds_f32(buf + 2 * XB + ((is_a ? 0 : TLQ) + 64 * pr) * 4, (is_a ? LSE : DLT) + src);
-    }
-  };
-  constexpr int OPS = 2 * QT * NSUB;
-  auto wait_oldest = [&](int younger) {
-    if (younger <= 0)
-      vmcnt<0>();
-    else if (row_wave)
-      vmcnt<OPS + 1>();
-    else
-      vmcnt<OPS>();
-  };
-  // bounded spin on a mailbox counter (LDS); s_sleep between polls
-  const unsigned cnt_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + FL);
-  auto wait_count = [&](int idx, int target) {
-    for (int it = 0; it < (1 << 22); ++it) {
-      int v;
-      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cnt_lds + 4 * idx) : "memory");
-      if (__builtin_amdgcn_readfirstlane(v) >= target) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-  };
-  auto post_count = [&](int idx, int value) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\tds_write_b32 %0, %1" ::"v"(cnt_lds + 4 * idx), "v"(value) : "memory");
-  };
-  // the S (wave a) or dP' (wave b) chain of 32-query block blk of a tile
-  auto chain = [&](const char* tb, int blk, f32x4 (&st)[2][2]) {
-    const int sq = blk >> 1, qb = blk & 1;
-    const char* lx = tb + (is_a ? 0 : XB) + sq * NSUB * SUB;
-    const float* lc = (const float*)(tb + 2 * XB) + (is_a ? 0 : TLQ) + 64 * sq + 32 * qb;
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      const f32x4 L = *(const f32x4*)(lc + 16 * qs + 4 * g);
-      st[qs][0] = st[qs][1] = L;
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        const bf16x8 ax = frag_row16(lx + (ks >> 1) * SUB, 32 * qb + 16 * qs, ks & 1, lane);
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
-          st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax, bo[t2][ks], st[qs][t2], 0, 0, 0);
-      }
-  };
-  // dV^T += dO^T P (wave a) or dK^T += Q^T dS' (wave b) for block blk
-  auto grads = [&](const char* tb, int blk, const f32x4 (&st)[2][2]) {
-    const int sq = blk >> 1, qb = blk & 1;
-    const char* lt = tb + (is_a ? XB : 0) + sq * NSUB * SUB;
-    bf16x8 bf[2];
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) bf[t2] = pack_perm(st[0][t2], st[1][t2]);
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      const bf16x8 at = frag_tr16(lt + (ds >> 2) * SUB, 32 * qb, ds & 3, lane);
-#pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2)
-        acc[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at, bf[t2], acc[ds][t2], 0, 0, 0);
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < NBUF - 1; ++i)
-    if (i < ntiles) issue(smem + i * BUF, qbeg + (long)i * TLQ);
-  wait_oldest(min(NBUF - 2, ntiles - 1));
-  OWLK_BARRIER();
-
-  int nblk = 0;  // blocks exchanged so far by this pair
-  char* mbox = smem + MB + pr * NPS * PSLOT;
-  for (int t = 0; t < ntiles; ++t) {
-    const long q0 = qbeg + (long)t * TLQ;
-    if (t + NBUF - 1 < ntiles) issue(smem + ((t + NBUF - 1) % NBUF) * BUF, q0 + (long)(NBUF - 1) * TLQ);
-    const char* tb = smem + (t % NBUF) * BUF;
-
-    int kind = TILE_FULL;
-    if (t < full.lo || t >= full.hi) {
-      const long qlast = (q0 + TLQ - 1 < p.Lq ? q0 + TLQ - 1 : p.Lq - 1);
-      kind = TILE_EMPTY;
-      if (wave_live) kind = classify(m, b, frame_of(m, q0), frame_of(m, qlast), wfk0, wfk1);
-      if (kind == TILE_FULL && (q0 + TLQ > p.Lq || kw0 + 32 > p.Lkv)) kind = TILE_PARTIAL;
-    }
-    kind = __builtin_amdgcn_readfirstlane(kind);
-
-    if (kind != TILE_EMPTY) {
-      if (is_a) {
-        const bool masked = kind == TILE_PARTIAL;
-#pragma unroll
-        for (int blk = 0; blk < NB; ++blk) {
-          const int sq = blk >> 1, qb = blk & 1;
-          f32x4 st[2][2];
-          chain(tb, blk, st);
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
-          if (masked) {
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2) {
-              const unsigned long long bh =
-                  tile_bits(m, b, my_k[t2], my_k[t2] < p.Lkv, q0 + 64 * sq, p.Lq, false) >> (4 * g);
-              if (qb == 0) {
-                apply_bits4<0>(st[0][t2], bh, 0.f);
-                apply_bits4<16>(st[1][t2], bh, 0.f);
-              } else {
-                apply_bits4<32>(st[0][t2], bh, 0.f);
-                apply_bits4<48>(st[1][t2], bh, 0.f);
-              }
-            }
-          }
-          if (nblk >= NPS) wait_count(4 + pr, nblk - NPS + 1);  // the slot's previous block consumed
-          f32x4* slot = (f32x4*)(mbox + (nblk % NPS) * PSLOT) + lane;
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2) slot[64 * (2 * qs + t2)] = st[qs][t2];
-          post_count(pr, nblk + 1);
-          ++nblk;
-          grads(tb, blk, st);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        f32x4 cur[2][2], nxt[2][2];
-        chain(tb, 0, nxt);
-#pragma unroll
-        for (int blk = 0; blk < NB; ++blk) {
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2) cur[qs][t2] = nxt[qs][t2];
-          if (blk + 1 < NB) chain(tb, blk + 1, nxt);  // covers wave a's softmax of this block
-          wait_count(pr, nblk + 1);
-          const f32x4* slot = (const f32x4*)(mbox + (nblk % NPS) * PSLOT) + lane;
-          f32x4 pv[2][2];
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2) pv[qs][t2] = slot[64 * (2 * qs + t2)];
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) cur[qs][t2][r] *= pv[qs][t2][r];
-          post_count(4 + pr, nblk + 1);  // (after the reads returned: post_count waits lgkmcnt(0))
-          ++nblk;
-          grads(tb, blk, cur);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-    wait_oldest(min(NBUF - 2, ntiles - 2 - t));
-    OWLK_BARRIER();
-  }
-
-  // wave a: dV[key][d]; wave b: dK[key][d] (dS was accumulated negated); lane holds d = 16 ds + 4 g + r
-  const float osc = is_a ? 1.f : -p.scale;
-#pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2) {
-    if (my_k[t2] >= p.Lkv) continue;
-    bf16* po = is_a ? p.dv + b * p.sdvb + my_k[t2] * p.lddv + head * D + 4 * g
-                    : p.dk + b * p.sdkb + my_k[t2] * p.lddk + head * D + 4 * g;
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      bf16x4 a4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) a4[e] = (bf16)(acc[ds][t2][e] * osc);
-      *(bf16x4*)(po + 16 * ds) = a4;
     }
   }
 }
@@ -1380,9 +1148,9 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
       static const int v16 = getenv("OWLK_DKDV16") ? atoi(getenv("OWLK_DKDV16")) : 1;
       if (v16) {
         if (p.m.window <= 0)
-          hipLaunchKernelGGL((attn_bwd_dkdv16_k<64, 2>), grid, dim3(256), 0, s, p);
+          hipLaunchKernelGGL((attn_bwd_dkdv16_k<2>), grid, dim3(256), 0, s, p);
         else
-          hipLaunchKernelGGL((attn_bwd_dkdv16_k<64, 1>), grid, dim3(256), 0, s, p);
+          hipLaunchKernelGGL((attn_bwd_dkdv16_k<1>), grid, dim3(256), 0, s, p);
       } else if (p.m.window <= 0) {
         hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2>), grid, dim3(256), 0, s, p);
       } else {
@@ -1392,19 +1160,9 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
       // D 128 (one wave per SIMD): OWLK_DKDV128 = 0 plain, 1 pipelined FULL tiles, 2 128-row
       // query tiles (two-slot ring, 130 KiB), 3 both (default; global 134.7 -> 99.6 ms, local
       // 3.24 -> 2.70 ms at 20 heads x 98,304 tokens)
-      // 4 / 7: attn_bwd_dkdv_pair_k (16x16x32, wave pairs, two waves per SIMD), QT 1 / 2;
-      // 5 / 6: attn_bwd_dkdv16_k at one wave per SIMD, QT 2 / 1
       static const int v128 = getenv("OWLK_DKDV128") ? atoi(getenv("OWLK_DKDV128")) : 3;
-      const int v = v128 >= 4 ? v128 : (p.m.window <= 0 ? v128 : (v128 & 1));
-      if (v == 4)
-        hipLaunchKernelGGL((attn_bwd_dkdv_pair_k<D, 1>), grid, dim3(512), 0, s, p);
-      else if (v == 7)
-        hipLaunchKernelGGL((attn_bwd_dkdv_pair_k<D, 2>), grid, dim3(512), 0, s, p);
-      else if (v == 5)
-        hipLaunchKernelGGL((attn_bwd_dkdv16_k<D, 2>), grid, dim3(256), 0, s, p);
-      else if (v == 6)
-        hipLaunchKernelGGL((attn_bwd_dkdv16_k<D, 1>), grid, dim3(256), 0, s, p);
-      else if (v == 3)
+      const int v = p.m.window <= 0 ? v128 : (v128 & 1);
+      if (v == 3)
         hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2, true>), grid, dim3(256), 0, s, p);
       else if (v == 2)
         hipLaunchKernelGGL((attn_bwd_dkdv_k<D, 2, false>), grid, dim3(256), 0, s, p);
