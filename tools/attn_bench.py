@@ -35,8 +35,9 @@ def main():
     ap.add_argument("--dim", type=int, default=64, help="head_dim (dit_v4_5B: --heads 20 --dim 128)")
     ap.add_argument("--bwd-only", action="store_true")
     ap.add_argument("--windows", default="none,16", help="comma list of frame windows ('none' = global)")
+    ap.add_argument("--tpf", type=int, default=64, help="tokens per frame (mmdit_v2: 65)")
     args = ap.parse_args()
-    H, D, tpf = args.heads, args.dim, 64
+    H, D, tpf = args.heads, args.dim, args.tpf
     L = args.frames * tpf
     torch.manual_seed(0)
     qkv = torch.randn(1, L, 3 * H * D, device="cuda", dtype=torch.bfloat16)
