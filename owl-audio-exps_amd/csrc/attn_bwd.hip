@@ -1139,6 +1139,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
   }
 }
 
+// 128-row swept tiles (QT 2) pay the per-tile fixed costs once per two 64-row tiles; windowed sweeps
+// that are only a few tiles long lose more to their doubled mask-edge tiles (window 16 x 64 tokens:
+// +60 %), so QT 2 is taken for unwindowed masks and for windows of at least OWLK_BWD_QT2_MIN tokens
+// (default 4096: mmdit_v2's 256-frame layers)
+static bool long_sweep(const MaskP& m) {
+  static const long qt2_min = getenv("OWLK_BWD_QT2_MIN") ? atol(getenv("OWLK_BWD_QT2_MIN")) : 4096;
+  return m.window <= 0 || (long)m.window * m.tpf >= qt2_min;
+}
+
 template <int D>
 int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipStream_t s) {
   if (phases & 1) {
@@ -1147,7 +1156,7 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
       // the 16x16x32-MFMA variant by default (OWLK_DKDV16 = 0: 32x32x16): -7 % at the dit_v4 shape
       static const int v16 = getenv("OWLK_DKDV16") ? atoi(getenv("OWLK_DKDV16")) : 1;
       if (v16) {
-        if (p.m.window <= 0)
+        if (long_sweep(p.m))
           hipLaunchKernelGGL((attn_bwd_dkdv16_k<2>), grid, dim3(256), 0, s, p);
         else
           hipLaunchKernelGGL((attn_bwd_dkdv16_k<1>), grid, dim3(256), 0, s, p);
@@ -1178,7 +1187,7 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
     if constexpr (D == 64) {
       static const int v16 = getenv("OWLK_DQ16") ? atoi(getenv("OWLK_DQ16")) : 1;  // 16x16x32 variant (0: 32x32x16)
       if (v16) {
-        if (p.m.window <= 0)
+        if (long_sweep(p.m))
           hipLaunchKernelGGL((attn_bwd_dq16_k<64, 2>), grid, dim3(256), 0, s, p);
         else
           hipLaunchKernelGGL((attn_bwd_dq16_k<64, 1>), grid, dim3(256), 0, s, p);
