@@ -232,6 +232,7 @@ ATTN_CASES = [
     (1, 2, 12, 64, 4, "split"),
     (1, 2, 24, 64, None, False),  # unwindowed sweeps of 12 query tiles (dK/dV ping-pong ring wraps)
     (1, 1, 300, 1, None, False),  # token-causal: PARTIAL tiles on every diagonal, ragged end
+    (1, 2, 80, 64, 64, False),  # window of 4096 tokens: the backward's 128-row tiles (attn_bwd.hip long_sweep)
 ]
 
 
