@@ -880,8 +880,12 @@ __global__ __launch_bounds__(256, D == 64 ? (OWLK_DQ_INIT ? 2 : 3) : 2) void att
 // dQ^T += K^T dS in the permuted key order, K^T read by two ds_read_b64_tr_b16 per fragment.
 // D 128 (dit_v4_5B): two 64-column LDS sub-tiles per K / V tile, QT = 1 with a two-slot ring
 // (64 KiB per workgroup, two workgroups per CU).
-template <int D, int QT>
+// NT 16-query column tiles per wave (2: 32 queries, 3: 48): with 48, every K / V fragment read from
+// LDS and every tile's fixed costs feed 1.5x the MFMAs (as the forward's 64-query waves); 48 fits
+// two waves per SIMD only with the 32-key blocks taken as 16-key halves (the D 128 form), 64 does not.
+template <int D, int QT, int NT = 2>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
+  constexpr int TBQ = 4 * 16 * NT;  // queries per workgroup
   constexpr int NSUB = D / 64, NKD = D / 32, NDS = D / 16;
   constexpr int NBUF = (QT == 2 || D == 128) ? 2 : Cfg<D>::NBUF, TLK = TL * QT;
   constexpr int BUF = 2 * QT * NSUB * SUB;  // K [QT][NSUB] | V [QT][NSUB]
@@ -892,9 +896,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
   const BlockIds bid = xcd_block_ids();
   const long b = bid.z;
   const int head = bid.y;
-  const int ntq = (int)((p.Lq + TB - 1) / TB);
-  const long q0 = (long)(ntq - 1 - bid.x) * TB;
-  const long r0 = q0 + 32 * w;
+  const int ntq = (int)((p.Lq + TBQ - 1) / TBQ);
+  const long q0 = (long)(ntq - 1 - bid.x) * TBQ;
+  const long r0 = q0 + 16 * NT * w;
   const MaskP& m = p.m;
 
   const bf16* Q = p.q + b * p.sqb + head * D;
@@ -902,7 +906,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
   const bf16* V = p.v + b * p.svb + head * D;
   const bf16* dO = p.dout + b * p.sob + head * D;
 
-  const long qlast = (q0 + TB < p.Lq ? q0 + TB : p.Lq) - 1;
+  const long qlast = (q0 + TBQ < p.Lq ? q0 + TBQ : p.Lq) - 1;
   const int fq_lo = frame_of(m, q0 + m.q_offset), fq_hi = frame_of(m, qlast + m.q_offset);
   int lo_f;
   if (m.kv_lo) {
@@ -922,12 +926,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
   if (kv_end > p.Lkv) kv_end = p.Lkv;
   const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + TLK - 1) / TLK) : 0;
 
-  long my_q[2];
-  bool qok[2];
-  bf16x8 qf[2][NKD], df[2][NKD];  // [query tile][k step of 32 d]
-  f32x4 sinit[2], pinit[2];
+  long my_q[NT];
+  bool qok[NT];
+  bf16x8 qf[NT][NKD], df[NT][NKD];  // [query tile][k step of 32 d]
+  f32x4 sinit[NT], pinit[NT];
 #pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2) {
+  for (int t2 = 0; t2 < NT; ++t2) {
     my_q[t2] = r0 + 16 * t2 + c;
     qok[t2] = my_q[t2] < p.Lq;
 #pragma unroll
@@ -946,16 +950,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
     pinit[t2] = f32x4{-Dl, -Dl, -Dl, -Dl};
   }
   const bool wave_live = r0 < p.Lq;
-  const long wlast = (r0 + 31 < p.Lq ? r0 + 31 : p.Lq - 1);
+  const long wlast = (r0 + 16 * NT - 1 < p.Lq ? r0 + 16 * NT - 1 : p.Lq - 1);
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
   TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, TLK);
   if (!wave_live) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
 
-  f32x4 dq[NDS][2];  // [16-row d tile][query tile]
+  f32x4 dq[NDS][NT];  // [16-row d tile][query tile]
 #pragma unroll
-  for (int ds = 0; ds < NDS; ++ds) dq[ds][0] = dq[ds][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ds = 0; ds < NDS; ++ds)
+#pragma unroll
+    for (int t2 = 0; t2 < NT; ++t2) dq[ds][t2] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const GldsOff go_k = glds_offsets<SW_DUAL>(p.ldk, w, lane), go_v = glds_offsets<SW_ROW>(p.ldv, w, lane);
   auto issue = [&](char* buf, long c0) {
@@ -1007,23 +1013,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
       for (int sk = 0; sk < QT; ++sk) {
         const char* lk = tb + sk * NSUB * SUB;
         const char* lv = tb + (QT + sk) * NSUB * SUB;
-        unsigned long long bh[2] = {0ull, 0ull};
+        unsigned long long bh[NT] = {};
         if (masked) {
 #pragma unroll
-          for (int t2 = 0; t2 < 2; ++t2)
+          for (int t2 = 0; t2 < NT; ++t2)
             bh[t2] = tile_bits(m, b, my_q[t2], qok[t2], c0 + 64 * sk, p.Lkv, true) >> (4 * g);
         }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-          if constexpr (D == 128) {
+          if constexpr (D == 128 || NT >= 3) {
             // one 16-key row tile at a time (its S / dP chains over the four k steps, exp2, mask,
             // dS, half of the permuted B fragment): the 32-key form spills at two waves per SIMD
-            bf16x8 sf[2];
+            bf16x8 sf[NT];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-              f32x4 st[2], dp[2];
+              f32x4 st[NT], dp[NT];
 #pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2) {
+              for (int t2 = 0; t2 < NT; ++t2) {
                 st[t2] = sinit[t2];
                 dp[t2] = pinit[t2];
               }
@@ -1032,18 +1038,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
                 const bf16x8 ak = frag_row16<SW_DUAL>(lk + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
                 const bf16x8 av = frag_row16<SW_ROW>(lv + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
 #pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2) {
+                for (int t2 = 0; t2 < NT; ++t2) {
                   st[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t2][kd], st[t2], 0, 0, 0);
                   dp[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df[t2][kd], dp[t2], 0, 0, 0);
                 }
               }
 #pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2)
+              for (int t2 = 0; t2 < NT; ++t2)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) st[t2][r] = __builtin_amdgcn_exp2f(st[t2][r]);
               if (masked) {
 #pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2) {
+                for (int t2 = 0; t2 < NT; ++t2) {
                   if (kb == 0 && ks == 0) apply_bits4<0>(st[t2], bh[t2], 0.f);
                   if (kb == 0 && ks == 1) apply_bits4<16>(st[t2], bh[t2], 0.f);
                   if (kb == 1 && ks == 0) apply_bits4<32>(st[t2], bh[t2], 0.f);
@@ -1051,7 +1057,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
                 }
               }
 #pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2)
+              for (int t2 = 0; t2 < NT; ++t2)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sf[t2][4 * ks + r] = (bf16)(dp[t2][r] * st[t2][r]);
               __builtin_amdgcn_sched_barrier(0);  // register budget: one 16-key tile's S / dP live at a time
@@ -1060,16 +1066,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
             for (int ds = 0; ds < NDS; ++ds) {
               const bf16x8 akt = frag_tr16(lk + (ds >> 2) * SUB, 32 * kb, ds & 3, lane);
 #pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2)
+              for (int t2 = 0; t2 < NT; ++t2)
                 dq[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akt, sf[t2], dq[ds][t2], 0, 0, 0);
             }
             continue;
           }
-          f32x4 st[2][2], dp[2][2];  // [16-row key tile][query tile]
+          f32x4 st[2][NT], dp[2][NT];  // [16-row key tile][query tile]
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2) {
+            for (int t2 = 0; t2 < NT; ++t2) {
               st[ks][t2] = sinit[t2];
               dp[ks][t2] = pinit[t2];
             }
@@ -1080,7 +1086,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
               const bf16x8 ak = frag_row16<SW_DUAL>(lk + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
               const bf16x8 av = frag_row16<SW_ROW>(lv + (kd >> 1) * SUB, 32 * kb + 16 * ks, kd & 1, lane);
 #pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2) {
+              for (int t2 = 0; t2 < NT; ++t2) {
                 st[ks][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[t2][kd], st[ks][t2], 0, 0, 0);
                 dp[ks][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df[t2][kd], dp[ks][t2], 0, 0, 0);
               }
@@ -1088,12 +1094,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
+            for (int t2 = 0; t2 < NT; ++t2)
 #pragma unroll
               for (int r = 0; r < 4; ++r) st[ks][t2][r] = __builtin_amdgcn_exp2f(st[ks][t2][r]);
           if (masked) {
 #pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2) {
+            for (int t2 = 0; t2 < NT; ++t2) {
               if (kb == 0) {
                 apply_bits4<0>(st[0][t2], bh[t2], 0.f);
                 apply_bits4<16>(st[1][t2], bh[t2], 0.f);
@@ -1103,9 +1109,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
               }
             }
           }
-          bf16x8 sf[2];
+          bf16x8 sf[NT];
 #pragma unroll
-          for (int t2 = 0; t2 < 2; ++t2) {
+          for (int t2 = 0; t2 < NT; ++t2) {
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1116,7 +1122,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
           for (int ds = 0; ds < NDS; ++ds) {
             const bf16x8 akt = frag_tr16(lk + (ds >> 2) * SUB, 32 * kb, ds & 3, lane);
 #pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
+            for (int t2 = 0; t2 < NT; ++t2)
               dq[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(akt, sf[t2], dq[ds][t2], 0, 0, 0);
           }
         }
@@ -1126,7 +1132,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(BwdP p) {
     OWLK_BARRIER();
   }
 #pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2) {
+  for (int t2 = 0; t2 < NT; ++t2) {
     if (!qok[t2]) continue;
     bf16* pq = p.dq + b * p.sdqb + my_q[t2] * p.lddq + head * D + 4 * g;
 #pragma unroll
@@ -1186,7 +1192,14 @@ int launch_bwd(int phases, const BwdP& p, long B, int H, long Lq, long Lkv, hipS
     const dim3 grid((unsigned)((Lq + TB - 1) / TB), (unsigned)H, (unsigned)B);
     if constexpr (D == 64) {
       static const int v16 = getenv("OWLK_DQ16") ? atoi(getenv("OWLK_DQ16")) : 1;  // 16x16x32 variant (0: 32x32x16)
-      if (v16) {
+      // long sweeps: 48 queries per wave (3 x 16-query tiles, 192 per workgroup): global dQ 36.7 ->
+      // 34.2 ms at the dit_v4 shape; window 16 keeps 32 (1.07 -> 1.13 ms with 48).  OWLK_DQ_NT = 2
+      // forces 32 everywhere.
+      static const int nt = getenv("OWLK_DQ_NT") ? atoi(getenv("OWLK_DQ_NT")) : 3;
+      const dim3 grid3((unsigned)((Lq + 191) / 192), (unsigned)H, (unsigned)B);
+      if (v16 && nt == 3 && long_sweep(p.m)) {
+        hipLaunchKernelGGL((attn_bwd_dq16_k<64, 2, 3>), grid3, dim3(256), 0, s, p);
+      } else if (v16) {
         if (long_sweep(p.m))
           hipLaunchKernelGGL((attn_bwd_dq16_k<64, 2>), grid, dim3(256), 0, s, p);
         else
