@@ -488,20 +488,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_k(FwdP p) {
 // P feeds O^T += V^T P as the B operand in the permuted key order (pack_perm), V^T read by
 // frag_tr16.  Row sums stay per lane group until the epilogue (4 partial sums per query, added
 // across the groups there).  D 128 = two 64-column LDS sub-tiles per K / V tile.
-template <int D>
+template <int D, int NQ_ = D == 64 ? 4 : 2>
 struct F16Cfg {
-  static constexpr int NQ = D == 64 ? 4 : 2;  // 16-query tiles per wave
+  static constexpr int NQ = NQ_;              // 16-query tiles per wave
   static constexpr int QW = 16 * NQ;          // queries per wave
   static constexpr int QTW = 4 * QW;          // queries per workgroup
   static constexpr int NKD = D / 32, NDS = D / 16;
 };
-template <int D, bool RS>
+// KTT keys per swept tile: 64, or 128 (D 64 long sweeps: a two-slot ring of 32 KiB tiles, the
+// per-tile fixed costs paid once per 144 MFMAs)
+template <int D, bool RS, int KTT = KT, int NQ = F16Cfg<D>::NQ>
 __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   using C = Cfg<D>;
-  using F = F16Cfg<D>;
-  constexpr int NQ = F::NQ;
-  __shared__ __attribute__((aligned(16))) char smem[C::NBUF * C::TILEB + 16];
-  int& red_lo = *(int*)(smem + C::NBUF * C::TILEB);
+  using F = F16Cfg<D, NQ>;
+  constexpr int RH = KTT / KT;                        // 64-row halves of a tile
+  static_assert(RH == 1 || D == 64, "128-key tiles at D 64 only");
+  constexpr int NBUF = RH == 2 ? 2 : C::NBUF;
+  constexpr int TILEB = C::TILEB * RH, OPS = C::OPS * RH;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * TILEB + 16];
+  int& red_lo = *(int*)(smem + NBUF * TILEB);
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 15, g = lane >> 4;
   const BlockIds bid = xcd_block_ids();
@@ -534,8 +539,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   long kv_begin = (long)lo_f * m.tpf;
   long kv_end = ((long)hi_f + 1) * m.tpf;
   if (kv_end > p.Lkv) kv_end = p.Lkv;
-  kv_begin = (kv_begin / KT) * KT;
-  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + KT - 1) / KT) : 0;
+  kv_begin = (kv_begin / KTT) * KTT;
+  const int ntiles = kv_end > kv_begin ? (int)((kv_end - kv_begin + KTT - 1) / KTT) : 0;
 
   int my_q[NQ];  // < 2^31 (checked on the host)
   bf16x8 qf[NQ][F::NKD];  // [query tile][k step of 32 d], q' = bf16(q c)
@@ -575,7 +580,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   const long wlast = (r0 + F::QW - 1 < p.Lq ? r0 + F::QW - 1 : p.Lq - 1);
   const bool wave_live = r0 < p.Lq;
   const int wfq0 = frame_of(m, r0 + m.q_offset), wfq1 = frame_of(m, wlast + m.q_offset);
-  TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, KT);
+  TileRange full = full_range_kv(m, b, wfq0, wfq1, kv_begin, p.Lkv, KTT);
   if (!wave_live) full = TileRange{1, 0};
   full.lo = __builtin_amdgcn_readfirstlane(full.lo);
   full.hi = __builtin_amdgcn_readfirstlane(full.hi);
@@ -598,51 +603,59 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
 
   const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_TR>(p.ldv, w, lane);
+  // tile image: K [RH row halves of 64 keys][NSUB] | V [RH][NSUB]; at D 64 (NSUB 1) the RH halves of
+  // K (and of V) are one contiguous 128-B-row image, and every swizzle has period 16 rows
   auto issue = [&](char* buf, long c0) {
 #pragma unroll
-    for (int sb = 0; sb < C::NSUB; ++sb) {
-      if (c0 + KT <= p.Lkv) {
-        tile_glds_fast(buf + sb * SUB, K + c0 * p.ldk + 64 * sb, goff_k, w);
-        tile_glds_fast(buf + (C::NSUB + sb) * SUB, V + c0 * p.ldv + 64 * sb, goff_v, w);
-      } else {
-        tile_glds<SW_ROW>(buf + sb * SUB, K + 64 * sb, p.ldk, c0, p.Lkv, w, lane);
-        tile_glds<SW_TR>(buf + (C::NSUB + sb) * SUB, V + 64 * sb, p.ldv, c0, p.Lkv, w, lane);
+    for (int rh = 0; rh < RH; ++rh) {
+      const long cr = c0 + KT * rh;
+#pragma unroll
+      for (int sb = 0; sb < C::NSUB; ++sb) {
+        char* bk = buf + (rh * C::NSUB + sb) * SUB;
+        char* bv = buf + ((RH + rh) * C::NSUB + sb) * SUB;
+        if (cr + KT <= p.Lkv) {
+          tile_glds_fast(bk, K + cr * p.ldk + 64 * sb, goff_k, w);
+          tile_glds_fast(bv, V + cr * p.ldv + 64 * sb, goff_v, w);
+        } else {
+          tile_glds<SW_ROW>(bk, K + 64 * sb, p.ldk, cr, p.Lkv, w, lane);
+          tile_glds<SW_TR>(bv, V + 64 * sb, p.ldv, cr, p.Lkv, w, lane);
+        }
       }
     }
   };
   auto wait_oldest = [&](int younger) {
     if (younger > 0)
-      vmcnt<C::OPS>();
+      vmcnt<OPS>();
     else
       vmcnt<0>();
   };
 #pragma unroll
-  for (int i = 0; i < C::NBUF - 1; ++i)
-    if (i < ntiles) issue(smem + i * C::TILEB, kv_begin + (long)i * KT);
-  wait_oldest(min(C::NBUF - 2, ntiles - 1));
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) issue(smem + i * TILEB, kv_begin + (long)i * KTT);
+  wait_oldest(min(NBUF - 2, ntiles - 1));
   OWLK_BARRIER();
 
   for (int t = 0; t < ntiles; ++t) {
-    const long c0 = kv_begin + (long)t * KT;
-    if (t + C::NBUF - 1 < ntiles)
-      issue(smem + ((t + C::NBUF - 1) % C::NBUF) * C::TILEB, c0 + (long)(C::NBUF - 1) * KT);
-    const char* lk = smem + (t % C::NBUF) * C::TILEB;
-    const char* lv = lk + C::NSUB * SUB;
+    const long c0 = kv_begin + (long)t * KTT;
+    if (t + NBUF - 1 < ntiles)
+      issue(smem + ((t + NBUF - 1) % NBUF) * TILEB, c0 + (long)(NBUF - 1) * KTT);
+    const char* lk = smem + (t % NBUF) * TILEB;
+    const char* lv = lk + RH * C::NSUB * SUB;
 
     int kind = TILE_FULL;
     if (t < full.lo || t >= full.hi) {
-      const long clast = (c0 + KT - 1 < p.Lkv ? c0 + KT - 1 : p.Lkv - 1);
+      const long clast = (c0 + KTT - 1 < p.Lkv ? c0 + KTT - 1 : p.Lkv - 1);
       kind = TILE_EMPTY;
       if (wave_live) kind = classify(m, b, wfq0, wfq1, frame_of(m, c0), frame_of(m, clast));
-      if (kind == TILE_FULL && c0 + KT > p.Lkv) kind = TILE_PARTIAL;
+      if (kind == TILE_FULL && c0 + KTT > p.Lkv) kind = TILE_PARTIAL;
     }
     kind = __builtin_amdgcn_readfirstlane(kind);
 
     if (kind != TILE_EMPTY) {
       const bool masked = kind == TILE_PARTIAL;
-      // per 32-key half kc: S^T of its two 16-key tiles x 4 query tiles, softmax, then O^T += V^T P
+      // per 32-key part kc: S^T of its two 16-key tiles x 4 query tiles, softmax, then O^T += V^T P
 #pragma unroll
-      for (int kc = 0; kc < 2; ++kc) {
+      for (int kc = 0; kc < KTT / 32; ++kc) {
         f32x4 st[2][NQ];  // [16-key tile within the half][query tile]
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -712,7 +725,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
         __builtin_amdgcn_sched_barrier(0);  // one key half's S / P live at a time (register budget)
       }
     }
-    wait_oldest(min(C::NBUF - 2, ntiles - 2 - t));
+    wait_oldest(min(NBUF - 2, ntiles - 2 - t));
     OWLK_BARRIER();
   }
 
@@ -955,6 +968,24 @@ void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   static const int f16_128 = getenv("OWLK_FWD16_128") ? atoi(getenv("OWLK_FWD16_128")) : 1;
   if (f16 && p.bound > 0.f && (D == 64 || f16_128)) {
     const dim3 g2((unsigned)((p.Lq + F16Cfg<D>::QTW - 1) / F16Cfg<D>::QTW), grid.y, grid.z);
+    // long sweeps (unwindowed, or windows of >= 4096 tokens): D 64 takes 128-key tiles (global 24.46
+    // -> 24.00 ms at the dit_v4 shape; OWLK_FWD_KT128 = 0 turns it off), D 128 48 queries per wave
+    // (global 46.5 -> 41.5 ms at the dit_v4_5B shape; OWLK_FWD_NQ3 = 0); window 16 keeps the base form
+    const bool long_sweep = m.window <= 0 || (long)m.window * m.tpf >= 4096;
+    static const int kt128 = getenv("OWLK_FWD_KT128") ? atoi(getenv("OWLK_FWD_KT128")) : 1;
+    static const int nq3 = getenv("OWLK_FWD_NQ3") ? atoi(getenv("OWLK_FWD_NQ3")) : 1;
+    if constexpr (D == 64) {
+      if (rs && kt128 && long_sweep) {
+        hipLaunchKernelGGL((attn_fwd16_k<D, true, 128>), g2, dim3(256), 0, s, p);
+        return;
+      }
+    } else {
+      if (rs && nq3 && long_sweep) {
+        const dim3 g3((unsigned)((p.Lq + 191) / 192), grid.y, grid.z);
+        hipLaunchKernelGGL((attn_fwd16_k<D, true, KT, 3>), g3, dim3(256), 0, s, p);
+        return;
+      }
+    }
     if (rs)
       hipLaunchKernelGGL((attn_fwd16_k<D, true>), g2, dim3(256), 0, s, p);
     else

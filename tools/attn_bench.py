@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--heads", type=int, default=24)
     ap.add_argument("--dim", type=int, default=64, help="head_dim (dit_v4_5B: --heads 20 --dim 128)")
     ap.add_argument("--bwd-only", action="store_true")
+    ap.add_argument("--fwd-only", action="store_true")
     ap.add_argument("--windows", default="none,16", help="comma list of frame windows ('none' = global)")
     ap.add_argument("--tpf", type=int, default=64, help="tokens per frame (mmdit_v2: 65)")
     args = ap.parse_args()
@@ -64,6 +65,11 @@ def main():
         else:
             t_f = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o, score_bound=K.qk_norm_bound(D)), args.iters)
             t_f0 = timeit(lambda: K.attn_fwd(q, k, v, H, D, mask, o=o), args.iters)
+        if args.fwd_only:
+            print(f"window={window}: pairs/head={pairs / H:.4e}")
+            print(f"  fwd   {t_f:8.3f} ms  {4 * D * pairs / t_f / 1e9:7.1f} TF/s (4 D pairs; fixed-offset softmax)")
+            print(f"  fwd0  {t_f0:8.3f} ms  {4 * D * pairs / t_f0 / 1e9:7.1f} TF/s (running-max softmax)", flush=True)
+            continue
         t_kv = timeit(lambda: _lib.call("owlk_attn_bwd_dkdv", *args_b), args.iters)
         t_q = timeit(lambda: _lib.call("owlk_attn_bwd_dq", *args_b), args.iters)
         # dK/dV and dQ are independent given delta: the pair back to back on one stream against dQ
