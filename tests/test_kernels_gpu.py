@@ -246,7 +246,7 @@ def _docs(B, nf, docs):
     return doc
 
 
-@pytest.mark.parametrize("case,D", [(c, 64) for c in ATTN_CASES] + [(ATTN_CASES[i], 128) for i in (0, 2, 4, 6)])
+@pytest.mark.parametrize("case,D", [(c, 64) for c in ATTN_CASES] + [(ATTN_CASES[i], 128) for i in (0, 2, 4, 6, 12)])
 def test_attention_fwd_bwd(case, D):
     """dit_v4 / mmdit heads are 64 wide, dit_v4_5B heads 128 (d 2560 / 20 heads)."""
     k = K()
