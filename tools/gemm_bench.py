@@ -25,6 +25,10 @@ def timeit(fn, iters=5):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--wgrad-only", action="store_true", help="only the split-K weight-gradient GEMMs, no hipBLASLt")
+    args = ap.parse_args()
     T, d = 98304, 1536
     torch.manual_seed(0)
     r = lambda *s: (torch.randn(*s, device="cuda") * 0.5).to(torch.bfloat16)
@@ -41,6 +45,8 @@ def main():
         ("out dW", r(T, d), r(T, d), True, True),
     ]
     for name, A, B, at, bt in cases:
+        if args.wgrad_only and not at:
+            continue
         M = A.shape[1] if at else A.shape[0]
         N = B.shape[1] if bt else B.shape[0]
         Kd = A.shape[0] if at else A.shape[1]
@@ -49,11 +55,16 @@ def main():
             ours = timeit(lambda: K.gemm_wgrad(A, B))
         else:
             ours = timeit(lambda: K.gemm(A, B, b_trans=bt))
+        if args.wgrad_only:
+            print(f"{name:8s} [{M}x{N}x{Kd}]  owlk {ours:7.3f} ms {fl / ours / 1e9:7.1f} TF/s", flush=True)
+            continue
         Am = A.T if at else A
         Bm = B if bt else B.T
         ref = timeit(lambda: torch.matmul(Am, Bm))
         print(f"{name:8s} [{M}x{N}x{Kd}]  owlk {ours:7.3f} ms {fl / ours / 1e9:7.1f} TF/s | "
               f"hipBLASLt {ref:7.3f} ms {fl / ref / 1e9:7.1f} TF/s", flush=True)
+    if args.wgrad_only:
+        return
     # fused epilogues at the block's shapes (fused.py): fc1 + SiLU, fc1 dX + dSiLU + bias-grad colsum,
     # out-proj / fc2 + gate + residual
     x, w1, w2, wo = r(T, d), r(4 * d, d), r(d, 4 * d), r(d, d)
