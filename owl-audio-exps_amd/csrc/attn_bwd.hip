@@ -14,10 +14,6 @@
 #include "attn_common.hpp"
 
 
-#ifndef OWLK_DKDV_ORDER
-#define OWLK_DKDV_ORDER 0
-#endif
-
 namespace {
 
 constexpr int TB = 128;              // rows owned by a workgroup (4 waves x 32)
@@ -539,42 +535,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(BwdP p) {
             st[qs][0] = st[qs][1] = L;
             dp[qs][0] = dp[qs][1] = Dl;
           }
-#if OWLK_DKDV_ORDER
-          // the S chain first, then the dP chain: the exp2 of P issues in the gaps of the dP MFMAs
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int qs = 0; qs < 2; ++qs) {
-              const bf16x8 aq = frag_row16(lq, 32 * qb + 16 * qs, ks, lane);
-#pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2)
-                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kf[t2][ks], st[qs][t2], 0, 0, 0);
-            }
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int qs = 0; qs < 2; ++qs) {
-              const bf16x8 ad = frag_row16(ld, 32 * qb + 16 * qs, ks, lane);
-#pragma unroll
-              for (int t2 = 0; t2 < 2; ++t2)
-                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vf[t2][ks], dp[qs][t2], 0, 0, 0);
-            }
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
-#if OWLK_DKDV_ORDER == 1
-          // pin the order: the 8 S MFMAs, then each dP MFMA followed by two exp2 (VALU)
-          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-          }
-#endif
-#else
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -593,7 +553,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(BwdP p) {
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
               for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
-#endif
           if (masked) {
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2) {
@@ -607,42 +566,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(BwdP p) {
             }
           }
           bf16x8 pf[2], sf[2];
-#if OWLK_DKDV_ORDER
-          // P packed first: the dV MFMAs run while dS = P o (dP - delta) is formed and packed
-#pragma unroll
-          for (int t2 = 0; t2 < 2; ++t2) pf[t2] = pack_perm(st[0][t2], st[1][t2]);
-#pragma unroll
-          for (int ds = 0; ds < 4; ++ds) {
-            const bf16x8 ado = frag_tr16(ld, 32 * qb, ds, lane);
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-              dv[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pf[t2], dv[ds][t2], 0, 0, 0);
-          }
-#pragma unroll
-          for (int t2 = 0; t2 < 2; ++t2) {
-#pragma unroll
-            for (int qs = 0; qs < 2; ++qs)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) dp[qs][t2][r] *= st[qs][t2][r];
-            sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
-          }
-#if OWLK_DKDV_ORDER == 1
-          // pin: P pack (8 cvt), then each dV MFMA followed by its share of the dS VALU (16 mul + 8 cvt)
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 1);
-          }
-#endif
-#pragma unroll
-          for (int ds = 0; ds < 4; ++ds) {
-            const bf16x8 aqt = frag_tr16(lq, 32 * qb, ds, lane);
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-              dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
-          }
-#else
 #pragma unroll
           for (int t2 = 0; t2 < 2; ++t2) {
 #pragma unroll
@@ -662,7 +585,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(BwdP p) {
               dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
             }
           }
-#endif
         }
       }
     }
