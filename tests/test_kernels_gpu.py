@@ -833,7 +833,7 @@ def test_fused_adamw_matches_torch(eps, wd):
 
 @pytest.mark.parametrize("M,N,Kd", [(64, 6144, 1536), (64, 1536, 6144), (128, 4608, 1536), (72, 256, 512),
                                     (1, 1536, 1536), (2, 3072, 128), (16, 256, 64), (40, 1536, 4608),
-                                    (200, 1536, 1536)])
+                                    (200, 1536, 1536), (128, 10240, 2560)])
 def test_gemm_skinny_splitk_epilogues(M, N, Kd):
     """Skinny-M GEMMs (decode: one 64-token frame, a CFG pair, per-frame rows).  M <= 128 takes the
     one-launch decode plan (K chunks summed in order by each tile's last workgroup, arrival counters
