@@ -402,6 +402,11 @@ def main():
                            "tokens / max-over-ranks time); the per-GPU figure is tokens_per_s_per_gpu",
                "step_mfma_frac": round(value * (FLOP_PER_TOKEN if headline else fpt) / world / PEAK_BF16, 4),
                "roofline": roof, "cpu_baseline": cpu}
+        if kernels:  # the micro-step's largest kernel families by time (same HIP-event pass as roofline)
+            out["kernel_rates"] = {k: {"launches": n_, "avg_ms": round(ms_ / n_, 3),
+                                       "tflops": round(fl_ / max(ms_, 1e-9) / 1e9, 1),
+                                       "frac": round(fl_ / max(ms_, 1e-9) * 1e3 / PEAK_BF16, 4)}
+                                   for k, (n_, ms_, fl_) in kernels[:8] if fl_ > 0}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
