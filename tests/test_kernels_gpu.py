@@ -233,6 +233,7 @@ ATTN_CASES = [
     (1, 2, 24, 64, None, False),  # unwindowed sweeps of 12 query tiles (dK/dV ping-pong ring wraps)
     (1, 1, 300, 1, None, False),  # token-causal: PARTIAL tiles on every diagonal, ragged end
     (1, 2, 80, 64, 64, False),  # window of 4096 tokens: the backward's 128-row tiles (attn_bwd.hip long_sweep)
+    (2, 2, 70, 64, 64, "split"),  # the same long-sweep tile forms on PARTIAL tiles of the general document mask
 ]
 
 
@@ -246,7 +247,7 @@ def _docs(B, nf, docs):
     return doc
 
 
-@pytest.mark.parametrize("case,D", [(c, 64) for c in ATTN_CASES] + [(ATTN_CASES[i], 128) for i in (0, 2, 4, 6, 12)])
+@pytest.mark.parametrize("case,D", [(c, 64) for c in ATTN_CASES] + [(ATTN_CASES[i], 128) for i in (0, 2, 4, 6, 12, 13)])
 def test_attention_fwd_bwd(case, D):
     """dit_v4 / mmdit heads are 64 wide, dit_v4_5B heads 128 (d 2560 / 20 heads)."""
     k = K()
