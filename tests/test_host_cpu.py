@@ -359,6 +359,51 @@ def test_gemm_splitk_workspace_query():
     assert q(6144, 1536, 98304, 1, 1, 1, 1, 0, 0.5) == 0       # beta other than 0 / 1
 
 
+def _gemm_args(M=64, N=64, K=64, batch=1, A=4096, C=8192, c_f32=0, epi=0, colsum=None):
+    return (M, N, K, batch, A, K, 0, 0, 4096, K, 0, 1, C, N, 0, c_f32, epi, 1.0, 0.0, None, None, 0, 0, None, 0, 0,
+            0, None, 0, 0, colsum, None, 0, None)
+
+
+def _attn_fwd_args(Lq=128, Lkv=128, D=64, doc=None, run_start=None):
+    # q, k, v, o at 16-byte-aligned stand-in addresses; nothing is dereferenced (the checks fail first)
+    return (4096, 3 * D, 0, 4096, 3 * D, 0, 4096, 3 * D, 0, 8192, D, 0, None, 1, 1, Lq, Lkv, D, D ** -0.5, 0.0, 64,
+            0, 1, 0, None, None, run_start, doc, 0, None)
+
+
+def _attn_bwd_args(Lq=128, Lkv=128, D=64):
+    p = (4096, D, 0)
+    return (p + p + p + p + (None, None) + p + p + p + (1, 1, Lq, Lkv, D, D ** -0.5, 64, 0, 1)
+            + (None, None, None, None, 0, None))
+
+
+@pytest.mark.parametrize("name,args,msg", [
+    ("owlk_gemm", _gemm_args(M=0), "gemm: bad sizes M=0"),
+    ("owlk_gemm", _gemm_args(N=12), "N=12 must be a multiple of 8"),
+    ("owlk_gemm", _gemm_args(A=4104), "16-byte aligned"),
+    ("owlk_gemm", _gemm_args(c_f32=1, epi=1), "fp32 output only with EPI_STORE"),
+    ("owlk_gemm", _gemm_args(batch=2, colsum=4096), "colsum needs batch 1"),
+    ("owlk_attn_fwd", _attn_fwd_args(D=96), "head_dim 96 not built"),
+    ("owlk_attn_fwd", _attn_fwd_args(Lq=0), "attn_fwd: bad sizes"),
+    ("owlk_attn_fwd", _attn_fwd_args(doc=4096), "doc mask needs run_start"),
+    ("owlk_attn_bwd", _attn_bwd_args(Lkv=256), "training shapes only"),
+    ("owlk_attn_bwd_dq", _attn_bwd_args(D=32), "head_dim 32 not built"),
+    ("owlk_adaln_fwd", (4096, 12, 4096, 4096, 12, 64, 128, 12, 8192, 12, None, None, None), "adaln_fwd: bad d=12"),
+    ("owlk_adaln_fwd", (4096, 64, 4096, 4096, 64, 64, 100, 64, 8192, 64, None, None, None), "T=100"),
+])
+def test_c_abi_rejects_bad_arguments(name, args, msg):
+    """The C ABI's error behaviour (owlk.h: every entry returns 0 or an error code with a message in
+    owlk_last_error()): shapes, layouts and alignments a kernel cannot take are refused on the host
+    before any HIP call, so this runs without a GPU; through the package binding they raise
+    RuntimeError (the reference's ops raise on unsupported shapes too, e.g. flex_attention)."""
+    from owl_wms import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libowlk.so not built (run __graft_entry__.build())")
+    assert getattr(_lib.lib(), name)(*args) != 0
+    assert msg in _lib.lib().owlk_last_error().decode()
+    with pytest.raises(RuntimeError, match=re.escape(msg)):
+        _lib.call(name, *args)
+
+
 @pytest.mark.parametrize("window", [None, 3])
 def test_mask_pairs_counts_documents(window):
     """The algorithmic FLOP count (allowed pairs only) with document arrays equals a
