@@ -234,6 +234,7 @@ ATTN_CASES = [
     (1, 1, 300, 1, None, False),  # token-causal: PARTIAL tiles on every diagonal, ragged end
     (1, 2, 80, 64, 64, False),  # window of 4096 tokens: the backward's 128-row tiles (attn_bwd.hip long_sweep)
     (2, 2, 70, 64, 64, "split"),  # the same long-sweep tile forms on PARTIAL tiles of the general document mask
+    (1, 2, 72, 65, 64, False),  # mmdit_v2's joint 65-token frames with a cut long window (64 x 65 >= 4096 tokens)
 ]
 
 
