@@ -183,6 +183,25 @@ int owlk_attn_bwd_dq(const void* q, long ldq, long sqb, const void* k, long ldk,
                      float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
                      const int* run_start, const int* doc, long fstride, void* stream);
 
+/* Single-pass backward (head_dim 64, unwindowed document-free masks, Lq == Lkv == L): the same
+ * outputs as owlk_attn_bwd from ONE kernel -- the compiled flex_attention backward of
+ * attn.py:13-16,106-109 is likewise one pass.  Each 256-key block forms S and dP once and adds its
+ * dQ part to a per-query-tile fp32 sum in the workspace in key-block order (ordered hand-off, no
+ * float atomics: dQ is bitwise reproducible).  ws: caller-owned, >= owlk_attn_bwd_fused_ws_bytes,
+ * 256-B aligned; the entry zeroes its header / flags itself (one memset on the stream).  variant:
+ * 0 = write-through (sc1) sums, any workgroup placement (default); bit 0 = a chain's sums kept in
+ * one XCD's L2 (plain stores, per-XCD queues); bit 1 = test mode: every contributor adds 1.0
+ * instead of its dQ part and the last one keeps the fp32 sum in ws (dQ not written).  After the
+ * call, ws int32 word 8 != 0 means a hand-off wait timed out (never expected). */
+long owlk_attn_bwd_fused_ws_bytes(long B, int H, long L, int head_dim);
+int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
+                        long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,
+                        const float* delta, void* dq, long lddq, long sdqb, void* dk, long lddk, long sdkb,
+                        void* dv, long lddv, long sdvb, long B, int H, long L, int head_dim, float scale,
+                        long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
+                        const int* run_start, const int* doc, long fstride, void* ws, long ws_bytes,
+                        int variant, void* stream);
+
 /* ---- Flow-matching noise + patchify (gamerft.py:92-95,107-108,52): x, z [BN, C, P] bf16,
  *   ts_raw [BN] fp32 (bf16-valued randn) -> xt, tgt token-major [BN*P, C]; ts_out = bf16 sigmoid */
 int owlk_flow_noise(const void* x, const void* z, const float* ts_raw, int C, int P, long BN, void* xt,

@@ -1,0 +1,629 @@
+// Frame-masked flash attention backward in ONE pass (gfx950, head_dim 64, unwindowed masks).
+//
+// Reference: the single compiled flex_attention backward behind attn.py:13-16, 106-109 (torch's
+// flex template forms dQ, dK and dV in one kernel).  Same math as attn_bwd.hip:
+//   dV = P^T dO,  dS = P o (dP - delta),  dK = scale dS^T Q,  dQ = scale dS K,
+// but every (key block, query tile) pair forms S and dP ONCE: 10 D FLOP executed per allowed pair
+// instead of the 14 D of the two-kernel form (its dQ kernel recomputes S and dP).
+//
+// Work item = 256 keys of one (batch, head) chain, held by an 8-wave workgroup (wave w: keys
+// 32 w .. 32 w + 31, as attn_bwd_dkdv16_k: S / dP with the key on the lane column, dK^T / dV^T
+// in registers).  The workgroup sweeps the 64-row query tiles its keys see in DECREASING order.
+// Per tile, dS goes to LDS as a [key][query] bf16 image; one tile later the 8 waves form
+// dQ^T[64 d x 64 q] = K^T dS^T over the item's 256 keys (K image in LDS, both operands read by
+// ds_read_b64_tr_b16) and add it to the tile's fp32 accumulator: an ORDERED hand-off -- key block
+// j adds to query tile i only after block j - 1 has (flag[i] >= j), so every tile receives its
+// partial sums in key-block order (bitwise reproducible, no float atomics).  The last contributor
+// of a tile (j == jhi(i)) writes bf16 dQ instead of the fp32 sum.
+//
+// Hand-off (cdna_hip_programming.md Guideline 16, R1 with a flag): every wave stores its part of
+// the accumulator write-through (sc1), drains it (s_waitcnt vmcnt(0)) before the workgroup barrier,
+// then ONE lane stores the flag (sc1).  Each consumer wave polls the flag with sc1 loads and reads
+// the accumulator with sc1 loads only after its own poll matched.  Variant bit 0 ("local") instead
+// keeps a chain's items on one XCD (per-XCD queues chosen by HW_REG_XCC_ID, no stealing) and stores
+// the accumulator with plain stores, so the sums stay in that XCD's L2; the A/B between the two is
+// the reason the variant exists.
+//
+// Pipelining: the accumulator of tile t + 1 is loaded in step t (issued mid-step, consumed as the
+// MFMA chain's initial value after the tile's dK/dV work), its new value is stored at the top of
+// step t - 1 and drained by that step's barrier; the flag goes out after it.  A successor block
+// therefore runs two tiles behind its predecessor.
+//
+// Forward progress: items are dequeued in increasing key-block order per chain from per-XCD atomic
+// queues; an item waits only on its chain predecessor, which a running workgroup dequeued earlier.
+// Spins are bounded by the real-time clock (error word in the workspace header).
+#include "attn_common.hpp"
+
+#define AS1 __attribute__((address_space(1)))
+#define AS3 __attribute__((address_space(3)))
+
+// timing-only experiment builds (tools/build_variant.sh -DOWLK_FUSED_EXP=n; results are WRONG):
+// bit 0: no hand-off (no flag polls, no sum loads); bit 1: no dQ products / stores either
+#ifndef OWLK_FUSED_EXP
+#define OWLK_FUSED_EXP 0
+#endif
+
+namespace {
+
+constexpr int FKB = 256;                                // keys per work item (8 waves x 32)
+constexpr int FQT = 64;                                 // query rows per swept tile
+constexpr int TILE_BYTES = 64 * 128;                    // 64 rows x 64 bf16, 128-B rows
+constexpr int RING_SLOT = 2 * TILE_BYTES + 2 * FQT * 4;  // Q | dO | lse2 | delta
+constexpr int NSLOT = 2;
+constexpr int KIMG_OFF = NSLOT * RING_SLOT;    // K of the item: 256 rows x 128 B
+constexpr int DS_OFF = KIMG_OFF + FKB * 128;   // two dS^T images [key][64 q] bf16
+constexpr int DS_BYTES = FKB * 128;
+constexpr int ACC_OFF = DS_OFF + 2 * DS_BYTES;  // per wave 2 KiB: its part of a tile's fp32 sum
+constexpr int FLAGL_OFF = ACC_OFF + 8 * 2048;    // per wave 256 B: a polled flag word (64 copies)
+constexpr int MISC_OFF = FLAGL_OFF + 8 * 256;
+constexpr int SMEM_BYTES = MISC_OFF + 16;
+constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
+constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word
+constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
+
+struct FusedP {
+  const bf16 *q, *k, *v, *dout;
+  const float *lse, *delta;  // [B, H, L]; lse in base 2 (attn_fwd)
+  bf16 *dq, *dk, *dv;
+  int ldq, ldk, ldv, ldo, lddq, lddk, lddv;  // token row strides (elements)
+  long sqb, skb, svb, sob, sdqb, sdkb, sdvb;  // batch strides
+  int L;                                      // Lq == Lkv
+  int H, nchain, ntiles, nkb;
+  int tpf, causal;    // the mask: frame = token / tpf; causal or none (no window, no documents)
+  unsigned magic;     // floor(2^32 / tpf) + 1 (exact frame division below 2^32 / tpf); 0 if tpf == 1
+  float scale, scale_log2;
+  int* hdr;    // dequeue counters / error word
+  int* flags;  // [nchain][ntiles] x FLAG_STRIDE
+  char* acc;   // [nchain][ntiles][ACC_TILE_BYTES]
+  int variant;
+};
+
+DEV unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
+
+// per-lane byte offset of frag_tr16(lds, row0, ds, lane) for any row0 that is a multiple of 16
+// (swz_dual repeats every 16 rows); the second ds_read_b64_tr_b16 of the fragment is 2 KiB further
+DEV int tr16_lane_off(int ds, int lane) {
+  const int c = lane & 15, g = lane >> 4;
+  const int x = 4 * g + (c >> 2);
+  const int ch = 2 * ds + ((c & 3) >> 1);
+  return x * 128 + ((ch ^ swz_dual(x)) << 4) + 8 * (c & 1);
+}
+
+// Every vector-memory access of the sweep goes through inline asm, and the waits are counted by
+// hand (vmcnt counts loads, LDS-DMA and stores in issue order).  A compiler-visible LDS-DMA makes
+// hipcc drain it (vmcnt(0)) before every ds_read_b64_tr_b16 (the builtin carries no memory operand),
+// which here would also drain the accumulator loads in flight; asm outputs get their waits through
+// "+v" operands of the s_waitcnt, so no consumer is scheduled above it.  The kernel uses m0 only
+// here (no other LDS-DMA, no dynamic register indexing).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+DEV unsigned lds_addr(const void* p) { return (unsigned)(uintptr_t)(const AS3 void*)p; }
+// one 16-B-per-lane LDS-DMA wave-instruction to the wave-uniform LDS byte address `lds`
+DEV void dma16(unsigned lds, const void* src) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+}
+DEV void dma4(unsigned lds, const void* src) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+}
+// the hand-off's loads (sc1: past this CU's L1, cdna_hip_programming.md Guideline 16) land in LDS
+// too: a register destination of an asm load whose wait is a separate statement could be copied
+// by the compiler before the data arrives; these are read back by ds_read after vm_wait
+DEV void dma16_sc1(unsigned lds, const void* src) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1" ::"s"(lds), "v"(src)
+               : "memory", "m0");
+}
+DEV void dma4_sc1(unsigned lds, const void* src) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1" ::"s"(lds), "v"(src)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+template <int N>
+DEV void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+DEV int frame(const FusedP& p, int idx) { return p.magic ? (int)__umulhi((unsigned)idx, p.magic) : idx; }
+
+// last key block that query tile i sees (the mask is causal-by-frame or empty); every block
+// 0 .. jhi(i) sweeps tile i, each exactly once
+DEV int tile_jhi(const FusedP& p, int i) {
+  if (!p.causal) return p.nkb - 1;
+  const int ql = i * FQT + FQT - 1 < p.L ? i * FQT + FQT - 1 : p.L - 1;
+  const long kend = (long)(frame(p, ql) + 1) * p.tpf;
+  const int ke = kend < p.L ? (int)kend : p.L;
+  const int j = (ke - 1) / FKB;
+  return j < p.nkb - 1 ? j : p.nkb - 1;
+}
+
+// bounded poll of a flag word (every lane loads the same word: one request), sc1 loads
+DEV bool wait_flag(const int* f, int want, int* err) {
+  if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= want)
+    return true;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= want)
+      return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // >= 2 s at the 100 MHz clock
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    // after any timeout every later wait gives up at once (results are void; the word says so)
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
+      return false;
+  }
+}
+
+template <bool LOCAL, bool COUNTING>
+__global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
+  // ONE __shared__ object (see attn_bwd.hip: a second one makes hipcc drain the DMA ring)
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  int* sh_item = (int*)(smem + MISC_OFF);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  constexpr bool local = LOCAL, counting = COUNTING;
+  const unsigned xcc = xcc_id();
+  const int L = p.L;
+  char* kimg = smem + KIMG_OFF;
+  // this wave's quarter of dQ^T: d tile dt, query tiles qt0, qt0 + 1 (16 rows / columns each)
+  const int dt = w & 3, qt0 = 2 * (w >> 2);
+  const unsigned acc_lane = (unsigned)((2 * w) * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
+  const int offk = tr16_lane_off(dt, lane), offs0 = tr16_lane_off(qt0, lane), offs1 = tr16_lane_off(qt0 + 1, lane);
+
+  // per-lane LDS-DMA source offsets of a 64-row tile (wave w: rows 8 w .. 8 w + 7, one 1-KiB
+  // wave-instruction, swizzled source chunk)
+  const int drow = 8 * w + (lane >> 3);
+  const int dch = (lane & 7) ^ swz_dual(drow);
+  const unsigned offq = (unsigned)((drow * p.ldq + dch * 8) * 2), offd = (unsigned)((drow * p.ldo + dch * 8) * 2);
+
+  for (;;) {
+    // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local)
+    if (threadIdx.x == 0) {
+      int chain = -1, jj = 0;
+      for (int d = 0; d < (local ? 1 : 8) && chain < 0; ++d) {
+        const int x = (int)((xcc + d) & 7);
+        const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
+        if (cx == 0) continue;
+        const int total = cx * p.nkb;
+        if (__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) continue;
+        const int n = __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n < total) {
+          chain = x + 8 * (n % cx);
+          jj = n / cx;
+        }
+      }
+      sh_item[0] = chain;
+      sh_item[1] = jj;
+    }
+    __syncthreads();
+    const int chain = __builtin_amdgcn_readfirstlane(sh_item[0]);
+    const int j = __builtin_amdgcn_readfirstlane(sh_item[1]);
+    if (chain < 0) return;
+
+    const int b = chain / p.H;
+    const int head = chain % p.H;
+    const bf16* Q = p.q + b * p.sqb + head * 64;
+    const bf16* K = p.k + b * p.skb + head * 64;
+    const bf16* V = p.v + b * p.svb + head * 64;
+    const bf16* dO = p.dout + b * p.sob + head * 64;
+    const float* LSE = p.lse + (long)chain * L;
+    const float* DLT = p.delta + (long)chain * L;
+    int* flg = p.flags + (long)chain * p.ntiles * FLAG_STRIDE;
+    const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+        p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES, (short)0, p.ntiles * ACC_TILE_BYTES, 0x00020000);
+    const int k0 = j * FKB, kw0 = k0 + 32 * w;
+    const int t_hi = p.ntiles - 1;
+    const int t_lo = p.causal ? (int)(((long)frame(p, k0) * p.tpf) / FQT) : 0;
+
+    // ---- K image of the item (unscaled K: the dQ^T A operand), 4 wave-instructions per wave
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 32 * w + 8 * i + (lane >> 3);
+      const int ch = (lane & 7) ^ swz_dual(row);
+      int gr = k0 + row;
+      gr = gr < L ? gr : L - 1;
+      dma16(lds_addr(kimg + (32 * w + 8 * i) * 128), K + (long)gr * p.ldk + ch * 8);
+    }
+    // ring: Q and dO 64-row tiles + the lse2 / delta rows (waves 0 / 1)
+    auto issue = [&](int t) {
+      char* buf = smem + (t & 1) * RING_SLOT;
+      const int q0 = t * FQT;
+      if (q0 + FQT <= L) {
+        dma16(lds_addr(buf + 8 * w * 128), (const char*)(Q + (long)q0 * p.ldq) + offq);
+        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), (const char*)(dO + (long)q0 * p.ldo) + offd);
+      } else {
+        int gr = q0 + drow;
+        gr = gr < L ? gr : L - 1;
+        dma16(lds_addr(buf + 8 * w * 128), Q + (long)gr * p.ldq + dch * 8);
+        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)gr * p.ldo + dch * 8);
+      }
+      if (w < 2) {
+        const int src = q0 + lane < L ? q0 + lane : L - 1;
+        dma4(lds_addr(buf + 2 * TILE_BYTES + w * FQT * 4), (w ? DLT : LSE) + src);
+      }
+    };
+
+    // this lane's two keys (column c of the wave's two 16-key tiles): k' = bf16(-c k), v' = -v
+    // (row constants in the accumulators, as attn_bwd_dkdv16_k)
+    int my_k[2];
+    bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      my_k[t2] = kw0 + 16 * t2 + c;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 kv = my_k[t2] < L ? *(const bf16x8*)(K + (long)my_k[t2] * p.ldk + 32 * ks + 8 * g) : bf16x8{};
+        bf16x8 vv = my_k[t2] < L ? *(const bf16x8*)(V + (long)my_k[t2] * p.ldv + 32 * ks + 8 * g) : bf16x8{};
+        float f[8], h8[8];
+        unpack8(kv, f);
+        unpack8(vv, h8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          f[e] *= -p.scale_log2;
+          h8[e] = -h8[e];
+        }
+        kf[t2][ks] = pack8(f);
+        vf[t2][ks] = pack8(h8);
+      }
+    }
+    // tile classes of this wave's 32 keys (frames wfk0 .. wfk1): FULL from the first query tile
+    // whose first frame is >= wfk1 (causal) up to the last whole tile, PARTIAL / EMPTY by frames
+    // outside that range
+    const bool wave_live = kw0 < L;
+    const int wfk0 = frame(p, kw0), wfk1 = frame(p, kw0 + 31 < L ? kw0 + 31 : L - 1);
+    int full_lo = p.causal ? (int)(((long)wfk1 * p.tpf + FQT - 1) / FQT) : 0;
+    int full_hi = L / FQT;  // exclusive: whole tiles only
+    if (!wave_live || kw0 + 32 > L) full_lo = full_hi = 0;
+    full_lo = __builtin_amdgcn_readfirstlane(full_lo);
+    full_hi = __builtin_amdgcn_readfirstlane(full_hi);
+
+    f32x4 dk[4][2], dv[4][2];
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) dk[ds][t2] = dv[ds][t2] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // store a finished dQ^T quarter of tile i: bf16 dQ by the tile's last contributor, else the fp32
+    // sum (sc1 write-through; plain in the local variant)
+    auto store_dq = [&](int i, const f32x4 (&vals)[2]) {
+      const bool last = j >= tile_jhi(p, i);
+      if (last && !counting) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int qrow = i * FQT + 16 * (qt0 + e) + c;
+          if (qrow < L) {
+            bf16x4 o4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o4[r] = (bf16)(vals[e][r] * -p.scale);  // dS accumulated negated
+            *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 16 * dt + 4 * g) = o4;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int off = (int)(i * ACC_TILE_BYTES + acc_lane + e * 1024);
+          if constexpr (local)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vals[e]), ars, off, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vals[e]), ars, off, 0, 16);
+        }
+      }
+    };
+    const char* accp = p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES + acc_lane;
+    char* accl = smem + ACC_OFF + w * 2048;  // this wave's landing zone (lane-linear, as acc_lane)
+    char* flagl = smem + FLAGL_OFF + w * 256;
+    auto load_acc = [&](int i) {  // -> accl, read back by read_acc after vm_wait
+      dma16_sc1(lds_addr(accl), accp + (long)i * ACC_TILE_BYTES);
+      dma16_sc1(lds_addr(accl + 1024), accp + (long)i * ACC_TILE_BYTES + 1024);
+    };
+    auto read_acc = [&](f32x4 (&vals)[2]) {
+      vals[0] = *(const f32x4*)(accl + lane * 16);
+      vals[1] = *(const f32x4*)(accl + 1024 + lane * 16);
+    };
+    // dQ^T quarter of tile i from its dS image (written in the step of tile i) over the 256 keys.
+    // frag_tr16 at row0 = 32 kk: the swizzle repeats every 16 rows, so one per-lane offset per
+    // 16-column group and immediate offsets kk * 4 KiB (+ 2 KiB for the second 4-row group)
+    auto dq_mfma = [&](int i, f32x4 (&a)[2]) {
+      if constexpr (counting) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[e][r] += 1.f;
+        return;
+      }
+      const char* kb = kimg + offk;
+      const char* sb0 = smem + DS_OFF + (i & 1) * DS_BYTES + offs0;
+      const char* sb1 = smem + DS_OFF + (i & 1) * DS_BYTES + offs1;
+#pragma unroll
+      for (int kk = 0; kk < FKB / 32; ++kk) {
+        const bf16x8 ak = join_tr(ds_read_tr16(kb + 4096 * kk), ds_read_tr16(kb + 4096 * kk + 2048));
+        const bf16x8 b0 = join_tr(ds_read_tr16(sb0 + 4096 * kk), ds_read_tr16(sb0 + 4096 * kk + 2048));
+        const bf16x8 b1 = join_tr(ds_read_tr16(sb1 + 4096 * kk), ds_read_tr16(sb1 + 4096 * kk + 2048));
+        a[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b0, a[0], 0, 0, 0);
+        a[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b1, a[1], 0, 0, 0);
+      }
+    };
+
+    issue(t_hi);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // dqc: the predecessor's sum of tile t, loaded in step t (after the first half of the tile, once
+    // the flag polled at the top has had time to arrive), the initial value of dQ(t)'s MFMA chain at
+    // the top of step t - 1; zeros for the chain's first block
+    // the predecessor's sum of the tile whose dQ is formed next lands in accl: loaded in the
+    // tile's own step (after its first half, once the flag polled at the top has had time to
+    // arrive), read back at the top of the next step; the chain's first block starts from zeros
+    bool ready = true;
+    auto dq_tile = [&](int i) {  // form, add and store dQ^T of tile i
+      if (OWLK_FUSED_EXP & 2) return;
+      f32x4 a[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      if (j > 0 && !(OWLK_FUSED_EXP & 1)) {
+        if (!ready) {
+          wait_flag(flg + i * FLAG_STRIDE, j, p.hdr + 8);
+          load_acc(i);
+        }
+        vm_wait<0>();  // the accumulator loads are the only vector-memory ops in flight
+        read_acc(a);
+      }
+      dq_mfma(i, a);
+      store_dq(i, a);
+    };
+    for (int t = t_hi; t >= t_lo; --t) {
+      const int q0 = t * FQT;
+      // top: dQ of tile t + 1 from its dS image (step t + 1), stored at once; this step's barrier
+      // drains the stores, then the flag goes out
+      if (t + 1 <= t_hi) dq_tile(t + 1);
+      // in issue order: dQ stores, the flag poll, the ring's LDS-DMA of tile t - 1
+      if (j > 0 && !(OWLK_FUSED_EXP & 1)) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE);
+      const bool dma = t - 1 >= t_lo;
+      if (dma) issue(t - 1);
+
+      const char* tb = smem + (t & 1) * RING_SLOT;
+      const char* lq = tb;
+      const char* ld = tb + TILE_BYTES;
+      const float* l2 = (const float*)(tb + 2 * TILE_BYTES);
+      const float* dlt = l2 + FQT;
+      char* dsw = smem + DS_OFF + (t & 1) * DS_BYTES;
+
+      int kind = TILE_FULL;
+      if (t < full_lo || t >= full_hi) {
+        const int fq1 = frame(p, q0 + FQT - 1 < L ? q0 + FQT - 1 : L - 1);
+        kind = !wave_live || (p.causal && wfk0 > fq1) ? TILE_EMPTY : TILE_PARTIAL;
+      }
+      kind = __builtin_amdgcn_readfirstlane(kind);
+      const bool masked = kind == TILE_PARTIAL;
+      unsigned long long bh[2] = {0ull, 0ull};
+      if (masked) {  // query rows [frame(key) tpf, L) (causal) / [0, L) of the tile, per key
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+          const long lo = p.causal ? (long)frame(p, my_k[t2]) * p.tpf : 0;
+          bh[t2] = my_k[t2] < L ? range_bits(lo - q0, (long)L - q0) >> (4 * g) : 0ull;
+        }
+      }
+      bool loads_out = false;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        if (kind == TILE_EMPTY) {
+          // no allowed pair for this wave's keys: its rows of the dS image are zero
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) {
+            const int r = 32 * w + 16 * t2 + c;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const int ch = 4 * qb + 2 * hh + (g >> 1);
+              *(bf16x4*)(dsw + r * 128 + ((ch ^ swz_dual(r)) << 4) + 8 * (g & 1)) = bf16x4{};
+            }
+          }
+        } else {
+          f32x4 st[2][2], dp[2][2];  // [16-row query tile][key tile]
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs) {
+            const int rowb = 32 * qb + 16 * qs + 4 * g;
+            const f32x4 Lr = *(const f32x4*)(l2 + rowb);
+            const f32x4 Dr = *(const f32x4*)(dlt + rowb);
+            st[qs][0] = st[qs][1] = Lr;
+            dp[qs][0] = dp[qs][1] = Dr;
+          }
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs) {
+              const bf16x8 aq = frag_row16(lq, 32 * qb + 16 * qs, ks, lane);
+              const bf16x8 ad = frag_row16(ld, 32 * qb + 16 * qs, ks, lane);
+#pragma unroll
+              for (int t2 = 0; t2 < 2; ++t2) {
+                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kf[t2][ks], st[qs][t2], 0, 0, 0);
+                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vf[t2][ks], dp[qs][t2], 0, 0, 0);
+              }
+            }
+#pragma unroll
+          for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) st[qs][t2][r] = __builtin_amdgcn_exp2f(-st[qs][t2][r]);
+          if (masked) {
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2) {
+              if (qb == 0) {
+                apply_bits4<0>(st[0][t2], bh[t2], 0.f);
+                apply_bits4<16>(st[1][t2], bh[t2], 0.f);
+              } else {
+                apply_bits4<32>(st[0][t2], bh[t2], 0.f);
+                apply_bits4<48>(st[1][t2], bh[t2], 0.f);
+              }
+            }
+          }
+          bf16x8 pf[2], sf[2];
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) {
+#pragma unroll
+            for (int qs = 0; qs < 2; ++qs)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) dp[qs][t2][r] *= st[qs][t2][r];
+            pf[t2] = pack_perm(st[0][t2], st[1][t2]);
+            sf[t2] = pack_perm(dp[0][t2], dp[1][t2]);
+          }
+          // -dS of this wave's keys into the [key][query] image: lane (c, g) holds queries
+          // 32 qb + 4 g .. + 3 (elements 0..3) and 32 qb + 16 + 4 g .. + 3 (elements 4..7) of key c
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2) {
+            const int r = 32 * w + 16 * t2 + c;
+            const bf16x4 lo4 = __builtin_shufflevector(sf[t2], sf[t2], 0, 1, 2, 3);
+            const bf16x4 hi4 = __builtin_shufflevector(sf[t2], sf[t2], 4, 5, 6, 7);
+            const int ch0 = 4 * qb + (g >> 1), ch1 = ch0 + 2;
+            *(bf16x4*)(dsw + r * 128 + ((ch0 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = lo4;
+            *(bf16x4*)(dsw + r * 128 + ((ch1 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = hi4;
+          }
+#pragma unroll
+          for (int ds = 0; ds < 4; ++ds) {
+            const bf16x8 ado = frag_tr16(ld, 32 * qb, ds, lane);
+            const bf16x8 aqt = frag_tr16(lq, 32 * qb, ds, lane);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2) {
+              dv[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pf[t2], dv[ds][t2], 0, 0, 0);
+              dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
+            }
+          }
+        }
+        if (qb == 0) {
+          if (j > 0 && !(OWLK_FUSED_EXP & 1)) {  // the flag polled at the top has had half a tile to arrive
+            if (!dma)
+              vm_wait<0>();
+            else if (w < 2)
+              vm_wait<3>();  // Q, dO and an lse2 / delta row
+            else
+              vm_wait<2>();
+            ready = __builtin_amdgcn_readfirstlane(*(const int*)(flagl + lane * 4)) >= j;
+            if (ready) {
+              load_acc(t);
+              loads_out = true;
+            }
+          }
+        }
+      }
+      // every wave: its dQ(t + 1) stores and the ring's tile t - 1 have landed (vmcnt counts in
+      // issue order; the accumulator loads of tile t, issued last, may stay in flight)
+      if (loads_out)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 1 <= t_hi && threadIdx.x == 0)
+        __hip_atomic_store(flg + (t + 1) * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
+    dq_tile(t_lo);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flg + t_lo * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // dK[key][d], dV[key][d]: this lane holds d = 16 ds + 4 g + r of its two keys
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      if (my_k[t2] >= L) continue;
+      bf16* pk = p.dk + b * p.sdkb + (long)my_k[t2] * p.lddk + head * 64 + 4 * g;
+      bf16* pv = p.dv + b * p.sdvb + (long)my_k[t2] * p.lddv + head * 64 + 4 * g;
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        bf16x4 a4, b4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a4[e] = (bf16)(dk[ds][t2][e] * -p.scale);  // dS was accumulated negated
+          b4[e] = (bf16)dv[ds][t2][e];
+        }
+        *(bf16x4*)(pk + 16 * ds) = a4;
+        *(bf16x4*)(pv + 16 * ds) = b4;
+      }
+    }
+  }
+}
+
+int fused_grid(int dev) {
+  static int cached[64] = {};
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (!cached[dev]) {
+    int cus = 0, per = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, attn_bwd_fused_k<false, false>, 512, 0);
+    cached[dev] = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+  }
+  return cached[dev];
+}
+
+}  // namespace
+
+static long fused_tiles(long L) { return (L + FQT - 1) / FQT; }
+
+extern "C" long owlk_attn_bwd_fused_ws_bytes(long B, int H, long L, int head_dim) {
+  if (head_dim != 64 || B <= 0 || H <= 0 || L <= 0) return 0;
+  const long nchain = B * H, nt = fused_tiles(L);
+  return HDR_BYTES + nchain * nt * (long)(FLAG_STRIDE * 4) + nchain * nt * (long)ACC_TILE_BYTES;
+}
+
+extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void* k, long ldk, long skb,
+                                   const void* v, long ldv, long svb, const void* dout, long ldo, long sob,
+                                   const float* lse, const float* delta, void* dq, long lddq, long sdqb, void* dk,
+                                   long lddk, long sdkb, void* dv, long lddv, long sdvb, long B, int H, long L,
+                                   int head_dim, float scale, long tpf, int window, int causal, const int* kv_lo,
+                                   const int* q_hi, const int* run_start, const int* doc, long fstride, void* ws,
+                                   long ws_bytes, int variant, void* stream) {
+  OWLK_REQUIRE(head_dim == 64, "attn_bwd_fused: head_dim %d not built (64)", head_dim);
+  OWLK_REQUIRE(tpf > 0 && L > 0 && B > 0 && H > 0, "attn_bwd_fused: bad sizes");
+  OWLK_REQUIRE(ldq < (1L << 31) && ldk < (1L << 31) && ldv < (1L << 31) && ldo < (1L << 31) && lddq < (1L << 31) &&
+                   lddk < (1L << 31) && lddv < (1L << 31),
+               "attn_bwd_fused: row strides too large");
+  OWLK_REQUIRE(window <= 0 && !kv_lo && !q_hi && !run_start && !doc,
+               "attn_bwd_fused: unwindowed, document-free masks only");
+  OWLK_REQUIRE(L < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_bwd_fused: sequence too long");
+  OWLK_REQUIRE(fused_tiles(L) * (long)ACC_TILE_BYTES < (1L << 31), "attn_bwd_fused: sequence too long");
+  OWLK_REQUIRE(B * H < (1L << 24), "attn_bwd_fused: too many heads");
+  const long need = owlk_attn_bwd_fused_ws_bytes(B, H, L, head_dim);
+  OWLK_REQUIRE(ws && ws_bytes >= need && (uintptr_t)ws % 256 == 0, "attn_bwd_fused: workspace (%ld bytes, 256-B aligned) needed",
+               need);
+  OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)dout | (uintptr_t)dq | (uintptr_t)dk |
+                (uintptr_t)dv) % 16 == 0,
+               "attn_bwd_fused: operands must be 16-byte aligned");
+  FusedP p;
+  p.q = (const bf16*)q; p.k = (const bf16*)k; p.v = (const bf16*)v; p.dout = (const bf16*)dout;
+  p.lse = lse; p.delta = delta;
+  p.dq = (bf16*)dq; p.dk = (bf16*)dk; p.dv = (bf16*)dv;
+  p.ldq = (int)ldq; p.ldk = (int)ldk; p.ldv = (int)ldv; p.ldo = (int)ldo;
+  p.lddq = (int)lddq; p.lddk = (int)lddk; p.lddv = (int)lddv;
+  p.sqb = sqb; p.skb = skb; p.svb = svb; p.sob = sob; p.sdqb = sdqb; p.sdkb = sdkb; p.sdvb = sdvb;
+  p.L = (int)L;
+  p.H = H;
+  p.nchain = (int)(B * H);
+  p.ntiles = (int)fused_tiles(L);
+  p.nkb = (int)((L + FKB - 1) / FKB);
+  p.tpf = (int)tpf;
+  p.causal = causal ? 1 : 0;
+  p.magic = tpf > 1 ? (unsigned)((1ull << 32) / (unsigned long long)tpf + 1) : 0u;
+  p.scale = scale;
+  p.scale_log2 = scale * 1.4426950408889634f;
+  p.hdr = (int*)ws;
+  p.flags = (int*)((char*)ws + HDR_BYTES);
+  p.acc = (char*)ws + HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4;
+  p.variant = variant;
+  hipStream_t s = (hipStream_t)stream;
+  // counters, error word and flags are zero on entry (one memset node, 16-B multiple from the start)
+  if (hipMemsetAsync(ws, 0, (size_t)(HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4), s) != hipSuccess)
+    return owlk::check_launch("attn_bwd_fused memset");
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const dim3 grid((unsigned)fused_grid(dev));
+  switch (variant & 3) {
+    case 0: hipLaunchKernelGGL((attn_bwd_fused_k<false, false>), grid, dim3(512), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((attn_bwd_fused_k<true, false>), grid, dim3(512), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((attn_bwd_fused_k<false, true>), grid, dim3(512), 0, s, p); break;
+    default: hipLaunchKernelGGL((attn_bwd_fused_k<true, true>), grid, dim3(512), 0, s, p); break;
+  }
+  return owlk::check_launch("attn_bwd_fused");
+}

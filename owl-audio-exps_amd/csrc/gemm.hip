@@ -1310,11 +1310,13 @@ struct SplitPlan {
   long splits, kchunk;
 };
 
+// frames: frame-strided operand rows (owlk_gemm_frames) -- only the 256^2 kernel reads them, so
+// neither the decode plan nor the skinny split-K plan may be taken
 static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
-                            float beta) {
+                            float beta, bool frames = false) {
   SplitPlan pl{SPLIT_NONE, 1, K};
   static const int use_decode = getenv("OWLK_GEMM_DECODE") ? atoi(getenv("OWLK_GEMM_DECODE")) : 1;
-  if (use_decode && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_T == 0 && K % 32 == 0 &&
+  if (use_decode && !frames && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_T == 0 && K % 32 == 0 &&
       ((M + DEC_T - 1) / DEC_T) * (N / DEC_T) <= kDecodeCounterBytes / 4 &&
       (epi == EPI_SILU || epi == EPI_GATE_RESID || epi == EPI_STORE)) {
     decode_split(M, N, K, pl.splits, pl.kchunk);  // kchunk field: sub-chunks per chunk
@@ -1322,7 +1324,7 @@ static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int
     return pl;
   }
   auto chunk = [&](long sp) { return ((K + sp - 1) / sp + BK - 1) / BK * BK; };
-  const long sk = skinny_splits(M, N, K, batch, c_f32, epi, beta);
+  const long sk = frames ? 1 : skinny_splits(M, N, K, batch, c_f32, epi, beta);
   if (sk > 1) {
     pl.kchunk = chunk(sk);
     pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
@@ -1403,7 +1405,8 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const long tiles128 = ((M + 127) / 128) * ((N + 127) / 128) * batch;
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   p.kchunk = K;
-  const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta);
+  const bool frames = p.a_fs || p.b_fs || p.c_fs;
+  const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta, frames);
   const long pws = split_ws_bytes(pl, M, N, batch);
   const bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
   if (pl.kind == SPLIT_DECODE && (pl.splits == 1 || have_ws)) return launch_decode(p, epi, ws, s);
@@ -1427,7 +1430,6 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32
   // atomics onto C, cleared first when beta = 0
   static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
-  const bool frames = p.a_fs || p.b_fs || p.c_fs;
   OWLK_REQUIRE(!frames || (fits256(M, N, K, a_trans, b_trans, c_f32, beta) && batch == 1 &&
                            (pl.kind == SPLIT_256 || pl.kind == SPLIT_NONE) &&
                            (pl.kind != SPLIT_256 || (have_ws && !atomic_splitk)) && pl.kchunk % FRAME_ROWS == 0),

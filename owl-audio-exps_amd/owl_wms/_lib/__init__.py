@@ -46,6 +46,9 @@ _SIGS = {
                            I, P, P, P, P, L, P],
     "owlk_attn_bwd_dq": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, L, I, F, L, I, I,
                          P, P, P, P, L, P],
+    "owlk_attn_bwd_fused_ws_bytes": [L, I, L, I],
+    "owlk_attn_bwd_fused": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, I, F, L, I, I,
+                            P, P, P, P, L, P, L, I, P],
     "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
     "owlk_unpatchify": [P, I, I, L, P, P],
     "owlk_mse": [P, P, L, F, P, P, I, P, P],
@@ -68,7 +71,7 @@ _SIGS = {
 
 # size queries; every other entry returns an int status
 _RESTYPES = {n: ctypes.c_long for n in ("owlk_gemm_splitk_bytes", "owlk_gemm_ws_bytes", "owlk_gemm_ws_counter_bytes",
-                                         "owlk_qk_rope_bwd_ws_bytes",
+                                         "owlk_qk_rope_bwd_ws_bytes", "owlk_attn_bwd_fused_ws_bytes",
                                         "owlk_colsum_ws_bytes", "owlk_ns_iterate_ws_bytes",
                                         "owlk_newton_schulz_ws_bytes")}
 

@@ -429,6 +429,34 @@ def _bwd_side_stream(device, D, mask):
     return s
 
 
+def fused_bwd_variant(D, mask):
+    """owlk_attn_bwd_fused variant for this layer, or None for the two-kernel backward.  The single
+    pass serves head_dim 64 with an unwindowed, document-free mask (dit_v4's global layers);
+    OWLK_BWD_FUSED = 0 turns it off, 1 (default) takes the write-through hand-off, 2 keeps each
+    chain's dQ sums in one XCD's L2 (include/owlk.h)."""
+    env = os.environ.get("OWLK_BWD_FUSED", "1")
+    if env == "0" or D != 64 or mask.window is not None or mask.arrays is not None or mask.q_offset != 0:
+        return None
+    return 1 if env == "2" else 0
+
+
+def attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, variant=0, ws=None):
+    """One pass of owlk_attn_bwd_fused (the caller has delta); returns the workspace (its fp32 dQ
+    sums and hand-off flags: tests read them in the counting variant)."""
+    B, L = q.shape[:2]
+    nb = lib().owlk_attn_bwd_fused_ws_bytes(B, H, L, D)
+    assert nb > 0, "attn_bwd_fused: shape not supported"
+    if ws is None:
+        ws = torch.empty(nb, device=q.device, dtype=torch.uint8)
+    call("owlk_attn_bwd_fused", ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
+         ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
+         ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),
+         ptr(dv), dv.stride(1), dv.stride(0), B, H, L, D, float(scale),
+         mask.tpf, 0, int(mask.causal), None, None, None, None, 0, ptr(ws), ws.numel(), int(variant), stream(),
+         key="attn_bwd_fused[wNone]", flops=lambda: 8.0 * D * H * B * mask_pairs(mask, L, L))
+    return ws
+
+
 def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
     """Backward of attn_fwd (training shapes: Lq == Lkv, q_offset 0); all tensors [B, L, cols]."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
@@ -438,6 +466,11 @@ def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
     delta = torch.empty(B, H, L, device=q.device, dtype=F32)
     assert o.is_contiguous() and do.is_contiguous() and o.shape == do.shape
     call("owlk_attn_delta", ptr(o), ptr(do), o.stride(1), B, L, H, D, ptr(delta), stream())
+    variant = fused_bwd_variant(D, mask)
+    if variant is not None:
+        # algorithmic FLOPs: the backward's 8 D per allowed pair (dV, dP, dK, dQ)
+        attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, variant)
+        return
     args = (ptr(q), q.stride(1), q.stride(0), ptr(k), k.stride(1), k.stride(0),
             ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
             ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),

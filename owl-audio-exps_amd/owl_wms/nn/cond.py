@@ -37,8 +37,17 @@ def _mlp_fwd(x, mlp, pad=0):
 
 
 def _wgrad_small_into(p, dy, x, k):
-    """weight gradient of a K = k < 16 input layer (x: its bf16 input rows, zero-padded wider)."""
+    """weight gradient of an input layer whose width k is not a multiple of 8 (x: its bf16 input rows,
+    zero-padded to a multiple of 8): owlk_small_k_wgrad for k <= 16 (angle_proj, button fc1), else
+    the padded input's split-K weight gradient cut to its first k columns."""
     sink = grad_sink(p)
+    if k > 16:
+        full = K.gemm_wgrad(dy, x)
+        if sink is None:
+            return full[:, :k].contiguous()
+        sink += full[:, :k]
+        grad_done(p)
+        return None
     if sink is None:
         return K.small_k_wgrad(dy, x, k)
     K.small_k_wgrad(dy, x, k, out=sink, beta=1.0)

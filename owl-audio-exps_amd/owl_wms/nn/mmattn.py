@@ -46,10 +46,17 @@ def _joint_views(j, n0, n1, cols):
     return K.frame_rows(j, n0, n1, 0, cols), j.view(F_, n0 + n1, cols)[:, n0, :]
 
 
-def _in_place_ok(d, n0, n1):
+def _in_place_ok(d, n0, n1, frames):
     """The joint layout is used in place (no frame_mux copies) where the video GEMMs tile by 256
-    (owlk_gemm_frames): mmdit_v2 (d 1536, 8x8 latents + 1 audio token per frame)."""
-    return n0 == K.FRAME_ROWS and n1 == 1 and d % 256 == 0
+    (owlk_gemm_frames): mmdit_v2 (d 1536, 8x8 latents + 1 audio token per frame), for more than
+    four frames of video rows (fewer take the frame_mux path, as decode-sized GEMMs)."""
+    return n0 == K.FRAME_ROWS and n1 == 1 and d % 256 == 0 and frames * n0 > 256
+
+
+def _lane_ok(inplace, frames, n1):
+    """The audio side stream only where its GEMMs (frames * n1 rows) stay off the decode plan, whose
+    workspace counters are shared per device (kernels._decode_ws)."""
+    return inplace and frames * n1 > 128
 
 
 _AUDIO_STREAMS = {}
@@ -107,8 +114,8 @@ class MMDiTBlockFn(torch.autograd.Function):
         ms = (c0.reshape(nf, 6 * d), c1.reshape(nf, 6 * d))
         ns = (n0, n1)
         W = [w[0:2], w[2:4]], [w[4:6], w[6:8]], [w[8:12], w[12:16]]  # qkv, out, mlp (fc1 w/b, fc2 w/b)
-        inplace = _in_place_ok(d, n0, n1)
-        lane = _AudioLane(x0.device, inplace)
+        inplace = _in_place_ok(d, n0, n1, nf)
+        lane = _AudioLane(x0.device, _lane_ok(inplace, nf, n1))
         h1, r1, qkv = [None, None], [None, None], [None, None]
         if inplace:  # each modality's qkv projection writes its rows of the joint frames directly
             qkvj = torch.empty(B * T, 3 * d, device=x0.device, dtype=BF16)
@@ -189,8 +196,8 @@ class MMDiTBlockFn(torch.autograd.Function):
 
         dcs = [torch.empty(nf, 6 * d, device=dout0.device, dtype=BF16) for _ in range(2)]  # d mods, bf16
         douts = (dout0.reshape(-1, d).to(BF16).contiguous(), dout1.reshape(-1, d).to(BF16).contiguous())
-        inplace = _in_place_ok(d, n0, n1)
-        lane = _AudioLane(o.device, inplace)
+        inplace = _in_place_ok(d, n0, n1, nf)
+        lane = _AudioLane(o.device, _lane_ok(inplace, nf, n1))
         if inplace:  # per-modality views of the joint o, and the joint dO the two dX GEMMs write into
             os_ = _joint_views(o.view(B * T, d), n0, n1, d)
             do = torch.empty(B * T, d, device=o.device, dtype=BF16)

@@ -1,0 +1,165 @@
+"""The single-pass attention backward (owlk_attn_bwd_fused, csrc/attn_bwd_fused.hip) against the
+fp32 oracle and the two-kernel backward, and its ordered dQ hand-off checked word by word.
+
+Reference: the one compiled flex_attention backward of attn.py:13-16, 106-109 (dQ, dK, dV from one
+pass); mask attn.py:24-62 without window / documents (dit_v4's global layers).  Tolerances: rel-L2
+<= 1e-2 against the fp32 oracle (SURVEY §8(c) per-op); the fused and the two-kernel bf16 results
+differ only in fp32 summation order and in the bf16 rounding of dS in the dQ product (<= 5e-3).
+"""
+import pytest
+import torch
+
+from oracle import ref_ops as R
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+FKB, FQT = 256, 64  # keys per work item, query rows per tile (attn_bwd_fused.hip)
+
+
+def K():
+    from owl_wms import kernels
+    return kernels
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(torch.bfloat16).to(DEV)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _needs_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from owl_wms._lib import lib
+    lib()
+
+
+def _inputs(B, H, L, D, seed):
+    q, kk, v, do = (rnd(B, L, H * D, seed=seed + i) for i in range(4))
+    return q, kk, v, do
+
+
+def _delta(o, do, H, D):
+    from owl_wms import _lib
+    B, L = o.shape[:2]
+    delta = torch.empty(B, H, L, device=DEV, dtype=torch.float32)
+    _lib.call("owlk_attn_delta", _lib.ptr(o), _lib.ptr(do), o.stride(1), B, L, H, D, _lib.ptr(delta), _lib.stream())
+    return delta
+
+
+def _hdr(ws):
+    return ws[:256].view(torch.int32).cpu()
+
+
+def _jhi(L, tpf, causal):
+    """last key block each 64-row query tile sees (frame-causal, unwindowed)"""
+    nkb = (L + FKB - 1) // FKB
+    out = []
+    for i in range((L + FQT - 1) // FQT):
+        if not causal:
+            out.append(nkb - 1)
+            continue
+        ql = min(i * FQT + FQT - 1, L - 1)
+        kend = min((ql // tpf + 1) * tpf, L)
+        out.append(min((kend - 1) // FKB, nkb - 1))
+    return torch.tensor(out)
+
+
+FUSED_CASES = [
+    # (B, H, n_frames, tpf, causal)
+    (1, 2, 8, 64, True),  # 2 key blocks, 8 query tiles
+    (2, 3, 20, 64, True),  # 6 chains (< 8 XCD queues), 5 key blocks
+    (1, 2, 7, 65, True),  # ragged end, frames across tile seams (455 tokens)
+    (1, 1, 300, 1, True),  # token-causal: PARTIAL diagonal tiles, ragged last key block
+    (1, 2, 40, 64, False),  # unmasked (every block sweeps every tile)
+    (2, 8, 48, 64, True),  # 16 chains x 12 key blocks
+]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("case", FUSED_CASES)
+def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
+    k = K()
+    B, H, nf, tpf, causal = case
+    D, L = 64, nf * tpf
+    q, kk, v, do = _inputs(B, H, L, D, 100)
+    mask = k.FrameMask(tpf, None, causal)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+    delta = _delta(o, do, H, D)
+    got = [torch.full_like(q, float("nan")) for _ in range(3)]
+    ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *got, D ** -0.5, variant)
+    torch.cuda.synchronize()
+    assert _hdr(ws)[8].item() == 0, "hand-off wait timed out"
+    monkeypatch.setenv("OWLK_BWD_FUSED", "0")
+    split = [torch.empty_like(q) for _ in range(3)]
+    k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, *split)
+    # fp32 oracle
+    qr, kr, vr = (t.cpu().float().view(B, L, H, D).transpose(1, 2).requires_grad_() for t in (q, kk, v))
+    m = R.frame_mask(L, L, tpf, None, None, causal=causal)
+    oref = R.attention(qr, kr, vr, m)
+    oref.backward(do.cpu().float().view(B, L, H, D).transpose(1, 2))
+    for name, g, s, ref in zip(("dq", "dk", "dv"), got, split, (qr.grad, kr.grad, vr.grad)):
+        assert torch.isfinite(g).all(), name
+        assert rel(g.view(B, L, H, D).transpose(1, 2), ref) < 1e-2, name
+        assert rel(g, s) < 5e-3, name
+
+
+@pytest.mark.parametrize("case", [(2, 8, 48, 64, True), (1, 2, 40, 64, False), (1, 1, 300, 1, True)])
+def test_attention_bwd_fused_deterministic(case):
+    """Every query tile receives its key blocks' dQ parts in key-block order, so two runs -- and the
+    write-through and the XCD-local hand-offs, which differ only in where the sums live -- give the
+    same bits."""
+    k = K()
+    B, H, nf, tpf, causal = case
+    D, L = 64, nf * tpf
+    q, kk, v, do = _inputs(B, H, L, D, 200)
+    mask = k.FrameMask(tpf, None, causal)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+    delta = _delta(o, do, H, D)
+    runs = []
+    for variant in (0, 0, 1, 1):
+        g = [torch.full_like(q, float("nan")) for _ in range(3)]
+        ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *g, D ** -0.5, variant)
+        torch.cuda.synchronize()
+        assert _hdr(ws)[8].item() == 0
+        runs.append(g)
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("shape", [(1, 24, 1536, 64, True), (2, 3, 20, 64, True), (1, 1, 300, 1, True),
+                                   (1, 2, 40, 64, False), (1, 8, 96, 65, True)])
+def test_attention_bwd_fused_handoff_counts(shape, variant):
+    """Counting form of the hand-off (variant bit 1): every key block adds 1.0 instead of its dQ
+    part and the last one keeps the fp32 sum, so each of the 4,096 words of every query tile's sum
+    must equal the number of key blocks that see the tile -- a stale read or a lost add anywhere
+    shows as a smaller count.  Checked at the full dit_v4 shape (24 heads x 98,304 tokens, 1,536
+    tiles x 384 key blocks per head, every XCD queue busy), for both hand-off forms; the flags end
+    at the same counts."""
+    k = K()
+    B, H, nf, tpf, causal = shape
+    D, L = 64, nf * tpf
+    q, kk, v, do = _inputs(B, H, L, D, 300)
+    mask = k.FrameMask(tpf, None, causal)
+    lse = torch.zeros(B, H, L, device=DEV)
+    delta = torch.zeros(B, H, L, device=DEV)
+    dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+    ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, dq, dk, dv, D ** -0.5, variant)
+    torch.cuda.synchronize()
+    assert _hdr(ws)[8].item() == 0, "hand-off wait timed out"
+    nchain, nt = B * H, (L + FQT - 1) // FQT
+    want = (_jhi(L, tpf, causal) + 1).to(DEV)
+    flags = ws[256:256 + nchain * nt * 64].view(torch.int32).view(nchain, nt, 16)[:, :, 0]
+    assert torch.equal(flags, want[None, :].to(torch.int32).expand(nchain, nt))
+    acc = ws[256 + nchain * nt * 64:256 + nchain * nt * (64 + FQT * 64 * 4)].view(torch.float32)
+    acc = acc.view(nchain, nt, FQT * 64)
+    bad = (acc != want[None, :, None].float()).sum().item()
+    assert bad == 0, f"{bad} accumulator words off"

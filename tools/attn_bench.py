@@ -101,6 +101,20 @@ def main():
         print(f"  dq    {t_q:8.3f} ms  {2 * D * pairs / t_q / 1e9:7.1f} TF/s alg (2 D pairs; 6 D executed: "
               f"{6 * D * pairs / t_q / 1e9:.1f})")
         print(f"  bwd   {t_kv + t_q:8.3f} ms  {8 * D * pairs / (t_kv + t_q) / 1e9:7.1f} TF/s alg", flush=True)
+        if K.fused_bwd_variant(D, mask) is not None or (D == 64 and window is None):
+            # single-pass backward (owlk_attn_bwd_fused): both hand-off forms, interleaved
+            nb = _lib.lib().owlk_attn_bwd_fused_ws_bytes(1, H, L, D)
+            ws = torch.empty(nb, device="cuda", dtype=torch.uint8)
+            t_fu = {0: [], 1: []}
+            for _ in range(2):
+                for var in (0, 1):
+                    t_fu[var].append(timeit(lambda: K.attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv,
+                                                                     D ** -0.5, var, ws), args.iters))
+            err = ws[:256].view(torch.int32)[8].item()
+            for var, nm in ((0, "write-through"), (1, "xcd-local")):
+                t = min(t_fu[var])
+                print(f"  fused {t:8.3f} ms  {8 * D * pairs / t / 1e9:7.1f} TF/s alg (8 D pairs; 10 D executed: "
+                      f"{10 * D * pairs / t / 1e9:.1f}) [{nm}: {t_fu[var]}] timeout word {err}", flush=True)
 
 
 if __name__ == "__main__":
