@@ -103,7 +103,8 @@ def cpu_baseline(steps=3):
 
 
 # kernel symbols (the 16x16x32 and 32x32x16 variants of each)
-PMC_KERNELS = {"attn_bwd_dkdv": "attn_bwd_dkdv(16)?_k", "attn_bwd_dq": "attn_bwd_dq(16)?_k", "attn_fwd": "attn_fwd"}
+PMC_KERNELS = {"attn_bwd_dkdv": "attn_bwd_dkdv(16)?_k", "attn_bwd_dq": "attn_bwd_dq(16)?_k", "attn_fwd": "attn_fwd",
+               "attn_bwd_fused": "attn_bwd_fused_k"}
 
 
 def pmc_traffic(args):
@@ -361,8 +362,9 @@ def main():
                 roof["traffic"] = round(tr["bytes"])
                 roof["traffic_unit"] = "bytes/launch (HBM, PMC, this run)"
                 # algorithmic bytes of one launch (either layer kind): Q, K, V, dO in and dK, dV out
-                # (bf16 [T, H D] each) plus lse2 and delta (fp32 [H, T])
-                alg = tokens * mc.d_model * 2 * 6 + tokens * mc.n_heads * 4 * 2 if dom == "attn_bwd_dkdv" else None
+                # (bf16 [T, H D] each) plus lse2 and delta (fp32 [H, T]); the single pass also writes dQ
+                n_io = {"attn_bwd_dkdv": 6, "attn_bwd_fused": 7}.get(dom)
+                alg = tokens * mc.d_model * 2 * n_io + tokens * mc.n_heads * 4 * 2 if n_io else None
                 roof["traffic_detail"] = {"fetch": round(tr["fetch"]), "write": round(tr["write"]),
                                           "launches": tr["launches"],
                                           **{kind: {"bytes_per_launch": round(tr[kind]["bytes"]),

@@ -10,7 +10,8 @@ Runs only where /root/reference exists.  Shims on top of make_golden's:
 Sampling runs under bf16 autocast, as the reference trainer's eval step does
 (rft_trainer.py:214-215).
 
-    python tests/golden/make_golden_sampler.py
+    python tests/golden/make_golden_sampler.py          # sampler_tiny.pt
+    python tests/golden/make_golden_sampler.py d128     # sampler_d128.pt (head_dim 128, round 4)
 """
 import os
 import sys
@@ -74,6 +75,27 @@ def gen_av():
             "av.dt": get_sd3_euler(2)}
 
 
+def gen_av_d128():
+    """AVCachingSamplerV2 at head_dim 128 (configs/dit_v4_5B.yml's attention width): the tiny D = 128
+    GameRFT of gamerft_d128.pt (d 256, 2 heads, base seed 1100), 4 context + 3 generated frames."""
+    cfg = G.tiny_video_cfg(d_model=256, n_heads=2, gradient_checkpointing=True)
+    model = det_init_(G.r_gamerft.GameRFT(cfg), base_seed=1100).eval()
+    B, ctx, new, C, s = 1, 4, 3, cfg.channels, cfg.sample_size
+    bf = G.bf16_exact
+    x = bf(det_tensor((B, ctx, C, s, s), 8300))
+    mouse = bf(det_tensor((B, ctx + new, 2), 8301))
+    g = torch.Generator().manual_seed(8302)
+    btn = (torch.rand((B, ctx + new, cfg.n_buttons), generator=g) < 0.5).float()
+    like = [bf(det_tensor((B, ctx, C, s, s), 8310))]
+    for f in range(new):
+        like += [bf(det_tensor((B, 1, C, s, s), 8320 + 2 * f)), bf(det_tensor((B, 1, C, s, s), 8321 + 2 * f))]
+    sampler = r_av.AVCachingSamplerV2(n_steps=2, cfg_scale=1.3, num_frames=new, noise_prev=0.2)
+    with G.inject_rng(randn_like=like), torch.autocast("cpu", dtype=torch.bfloat16):
+        out = sampler(model.core, x, mouse, btn)
+    return {"av128.in.x": x, "av128.in.mouse": mouse, "av128.in.btn": btn, "av128.noise": like,
+            "av128.out": out.float()}
+
+
 def gen_audio():
     cfg = G.audio_cfg()
     model = det_init_(G.r_audiorft.AudioRFT(cfg), base_seed=3000).eval()
@@ -89,6 +111,12 @@ def gen_audio():
 
 
 def main():
+    if sys.argv[1:] == ["d128"]:
+        out = gen_av_d128()
+        path = os.path.join(HERE, "sampler_d128.pt")
+        torch.save(out, path)
+        print(path, os.path.getsize(path) // 1024, "KiB", tuple(out["av128.out"].shape))
+        return
     out = gen_av()
     out.update(gen_audio())
     path = os.path.join(HERE, "sampler_tiny.pt")

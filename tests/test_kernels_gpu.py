@@ -964,3 +964,46 @@ def test_ema_fused_matches_foreach_lerp():
     sd = ema.state_dict()
     assert int(sd["step"]) == 5 and bool(sd["initted"]) and all("ema_model." + k in sd for k, _ in
                                                                   model.named_parameters())
+
+
+@pytest.mark.parametrize("F", [1, 2, 3, 4, 5])
+def test_gemm_frames_few_frames(F):
+    """owlk_gemm_frames on 1-5 frames (M = 64..320 frame-strided rows): such M would otherwise take
+    the decode (M <= 128) or skinny split-K (M <= 256) plans, which read plain rows; the frame-strided
+    form must stay on the 256^2 kernel.  A (frame rows of a joint [F x 65, 256] buffer) and C
+    (frame rows of a joint output) against the dense product."""
+    k = K()
+    n0, n1, Kd, N = 64, 1, 256, 256
+    joint = rnd(F * (n0 + n1), Kd, seed=300 + F)
+    B = rnd(N, Kd, seed=310 + F)
+    A = k.frame_rows(joint, n0, n1, 0, Kd)
+    rows = A.reshape(F * n0, Kd)
+    ref = rows.float() @ B.float().T
+    got = k.gemm(A, B.T.contiguous(), b_trans=True)  # the layout the MMDiT dX GEMMs use (mask 1)
+    assert rel(got, ref) < 1e-2
+    out_joint = torch.zeros(F * (n0 + n1), N, device=DEV, dtype=torch.bfloat16)
+    k.gemm(rows.contiguous(), B, out=k.frame_rows(out_joint, n0, n1, 0, N))
+    assert rel(k.frame_rows(out_joint, n0, n1, 0, N).reshape(F * n0, N), ref) < 1e-2
+    assert (out_joint.view(F, n0 + n1, N)[:, n0:] == 0).all()  # the audio rows are untouched
+
+
+@pytest.mark.parametrize("k_in", [20, 37])
+def test_mlp_custom_unaligned_wide_input(k_in):
+    """MLPCustom (mlp.py:20-24) on an input width > 16 that is not a multiple of 8 (a ButtonEmbedding
+    with more buttons than dit_v4's 11): the fc1 weight gradient takes the padded split-K path, not
+    owlk_small_k_wgrad (K <= 16); fwd and all grads against fp32 torch."""
+    from owl_wms.nn.mlp import MLPCustom
+    torch.manual_seed(5)
+    m = MLPCustom(k_in, 128, 64).cuda()
+    x = torch.randn(192, k_in, device=DEV).bfloat16().requires_grad_()
+    y = m(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    w1, b1, w2, b2 = (t.detach().float().requires_grad_() for t in (m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias))
+    xr = x.detach().float().requires_grad_()
+    yr = torch.nn.functional.silu(xr @ w1.T + b1) @ w2.T + b2
+    yr.backward(dy.float())
+    assert rel(y, yr) < 1e-2
+    for got, ref in ((x.grad, xr.grad), (m.fc1.weight.grad, w1.grad), (m.fc1.bias.grad, b1.grad),
+                     (m.fc2.weight.grad, w2.grad), (m.fc2.bias.grad, b2.grad)):
+        assert rel(got, ref) < 2e-2

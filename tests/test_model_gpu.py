@@ -284,24 +284,69 @@ def test_mmdit_joint_rows_in_place_equals_frame_mux(heads, monkeypatch):
     from owl_wms.models.gamerft_audio import GameRFTAudio
     from owl_wms.nn import mmattn
     cfg = dict(MMCFG, d_model=256, n_heads=heads, n_frames=8)
+    from owl_wms.utils.grad_reducer import GradReducer
     res = []
-    for inplace in (True, False):
+    # in place with the gradients written straight into GradReducer bucket views (the sinks the
+    # audio side stream's backward writes before lane.join, then reports), in place into .grad,
+    # and the frame_mux path
+    for inplace, reducer in ((True, True), (True, False), (False, False)):
         if not inplace:
             monkeypatch.setattr(mmattn, "_in_place_ok", lambda *a: False)
         m = det_init_(GameRFTAudio(model_config(**cfg)), base_seed=5100).cuda().train()
+        red = GradReducer(m.parameters(), world_size=1) if reducer else None
         B, n = 2, 8
         x = det_tensor((B, n, 32, 8, 8), 920).cuda().bfloat16()
         au = det_tensor((B, n, 16), 921).cuda().bfloat16()
         t = torch.sigmoid(det_tensor((B, n), 922)).cuda().bfloat16()
         mouse = det_tensor((B, n, 2), 923).cuda().bfloat16()
         btn = (det_tensor((B, n, 11), 924) > 0).cuda().bfloat16()
+        if red is not None:
+            red.begin(False)
         pv, pa = m.core(x, au, t, mouse, btn)
         (pv.float().square().mean() + pa.float().square().mean()).backward()
+        if red is not None:
+            red.finish()
         res.append((pv.float(), pa.float(),
-                    {k: p.grad.float() for k, p in m.named_parameters() if p.grad is not None}))
-    (v1, a1, g1), (v2, a2, g2) = res
+                    {k: p.grad.float().clone() for k, p in m.named_parameters() if p.grad is not None}))
+    (v0, a0, g0), (v1, a1, g1), (v2, a2, g2) = res
+    assert torch.equal(v0, v1) and torch.equal(a0, a1)
+    assert set(g1) <= set(g0)  # the reducer's bucket views exist for every parameter
+    for k in g1:  # same kernels, same order: the bucket-view writes give the same bits
+        assert torch.equal(g0[k], g1[k]), k
+    for k in set(g0) - set(g1):  # parameters the loss does not reach: zero in their bucket view
+        assert not g0[k].any(), k
     assert rel(v1, v2) < 1e-2 and rel(a1, a2) < 1e-2
     assert g1.keys() == g2.keys() and len(g1) > 20
+    for k in g2:
+        assert rel(g1[k], g2[k]) < 2e-2, (k, rel(g1[k], g2[k]))
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 5])
+def test_mmdit_few_frames_in_place_equals_frame_mux(n, monkeypatch):
+    """MMDiT forward + backward over 1-5 frames (mmdit_v2's d % 256 == 0 in-place layout; no KV
+    cache): at <= 4 frames the block takes the frame_mux path (its video GEMMs would be decode-
+    sized), at 5 the in-place one; either equals the frame_mux path."""
+    from owl_wms.configs import model_config
+    from owl_wms.models.gamerft_audio import GameRFTAudio
+    from owl_wms.nn import mmattn
+    cfg = dict(MMCFG, d_model=256, n_heads=4, n_frames=n)
+    res = []
+    for force_mux in (False, True):
+        if force_mux:
+            monkeypatch.setattr(mmattn, "_in_place_ok", lambda *a: False)
+        m = det_init_(GameRFTAudio(model_config(**cfg)), base_seed=5100).cuda().train()
+        x = det_tensor((1, n, 32, 8, 8), 930).cuda().bfloat16()
+        au = det_tensor((1, n, 16), 931).cuda().bfloat16()
+        t = torch.sigmoid(det_tensor((1, n), 932)).cuda().bfloat16()
+        mouse = det_tensor((1, n, 2), 933).cuda().bfloat16()
+        btn = (det_tensor((1, n, 11), 934) > 0).cuda().bfloat16()
+        pv, pa = m.core(x, au, t, mouse, btn)
+        (pv.float().square().mean() + pa.float().square().mean()).backward()
+        res.append((pv.float(), pa.float(), {k: p.grad.float() for k, p in m.named_parameters()
+                                             if p.grad is not None}))
+    (v1, a1, g1), (v2, a2, g2) = res
+    assert torch.isfinite(v1).all() and torch.isfinite(a1).all()
+    assert rel(v1, v2) < 1e-2 and rel(a1, a2) < 1e-2
     for k in g2:
         assert rel(g1[k], g2[k]) < 2e-2, (k, rel(g1[k], g2[k]))
 
@@ -341,6 +386,22 @@ def test_av_caching_sampler_vs_reference():
     assert out.shape == S["av.out"].shape
     assert rel(out[:, :4], S["av.out"][:, :4]) == 0.0
     assert rel(out[:, 4:], S["av.out"][:, 4:]) < 2e-2
+
+
+def test_av_caching_sampler_head_dim_128_vs_reference():
+    """AVCachingSamplerV2 (av_caching_v2.py:47-144) at head_dim 128 -- the attention width of
+    configs/dit_v4_5B.yml -- against the reference sampler's own latents (tests/golden/
+    make_golden_sampler.py d128: the gamerft_d128 weights, 4 context + 3 generated frames, 2 Euler
+    steps, CFG 1.3, bf16 autocast); through the D = 128 decode attention.  Within 2e-2."""
+    from owl_wms.sampling import get_sampler_cls
+    S = golden("sampler_d128.pt")
+    m = _model(d_model=256).eval()
+    sampler = get_sampler_cls("av_caching")(n_steps=2, cfg_scale=1.3, num_frames=3, noise_prev=0.2)
+    with _Draws(like=S["av128.noise"]):
+        out = sampler(m.core, S["av128.in.x"].cuda(), S["av128.in.mouse"].cuda(), S["av128.in.btn"].cuda())
+    assert out.shape == S["av128.out"].shape
+    assert rel(out[:, :4], S["av128.out"][:, :4]) == 0.0
+    assert rel(out[:, 4:], S["av128.out"][:, 4:]) < 2e-2
 
 
 def test_audio_caching_sampler_vs_reference():
