@@ -161,6 +161,7 @@ def pmc_traffic(args):
             fetch = 2.0 * sum(v["FETCH_SIZE"]) / n
             write = sum(v["WRITE_SIZE"]) / n
             out[k] = {"bytes": fetch + write, "fetch": fetch, "write": write, "launches": n}
+            n_global = sum(1 for i in range(n_layers) if i % every == 0)
             if n == n_layers:
                 # one launch per layer: the forward runs layers 0..L-1, the backward L-1..0; layer i is
                 # global iff i % local_idx == 0 (attn.py:151-153) -- report the two layer kinds apart
@@ -169,7 +170,32 @@ def pmc_traffic(args):
                     sel = [b for b, i in zip(per, layer) if (i % every == 0) == want]
                     if sel:
                         out[k][kind] = {"bytes": sum(sel) / len(sel), "launches": len(sel)}
+            elif n in (n_global, n_layers - n_global) and n_global != n_layers - n_global:
+                # one layer kind only (the single-pass backward serves the global layers, the
+                # two-kernel backward the local ones)
+                out[k]["global" if n == n_global else "local"] = {"bytes": sum(per) / n, "launches": n}
     return out
+
+
+# algorithmic bytes of one attention launch (either layer kind): bf16 [T, H D] operands in / out and
+# fp32 [H, T] rows (lse2, delta) -- (bf16 tensors, fp32 rows) per kernel
+ALG_IO = {"attn_fwd": (4, 1),          # Q, K, V in, O out; lse2 out
+          "attn_bwd_dkdv": (6, 2),     # Q, K, V, dO in, dK, dV out; lse2, delta in
+          "attn_bwd_dq": (5, 2),       # Q, K, V, dO in, dQ out; lse2, delta in
+          "attn_bwd_fused": (7, 2)}    # Q, K, V, dO in, dQ, dK, dV out; lse2, delta in
+
+
+def traffic_detail(kernel, tr, tokens, mc):
+    """the PMC bytes of one attention kernel beside its algorithmic bytes per launch"""
+    n_bf, n_f32 = ALG_IO.get(kernel, (0, 0))
+    alg = tokens * mc.d_model * 2 * n_bf + tokens * mc.n_heads * 4 * n_f32 if n_bf else None
+    return {"fetch": round(tr["fetch"]), "write": round(tr["write"]), "launches": tr["launches"],
+            **{kind: {"bytes_per_launch": round(tr[kind]["bytes"]), "launches": tr[kind]["launches"],
+                      **({"x_algorithmic": round(tr[kind]["bytes"] / alg, 2)} if alg else {})}
+               for kind in ("global", "local") if kind in tr},
+            **({"algorithmic_bytes_per_launch": alg} if alg else {}),
+            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, one micro-step; FETCH_SIZE x2 "
+                      "(gfx950)"}
 
 
 def microsteps(args):
@@ -361,20 +387,10 @@ def main():
             if tr:
                 roof["traffic"] = round(tr["bytes"])
                 roof["traffic_unit"] = "bytes/launch (HBM, PMC, this run)"
-                # algorithmic bytes of one launch (either layer kind): Q, K, V, dO in and dK, dV out
-                # (bf16 [T, H D] each) plus lse2 and delta (fp32 [H, T]); the single pass also writes dQ
-                n_io = {"attn_bwd_dkdv": 6, "attn_bwd_fused": 7}.get(dom)
-                alg = tokens * mc.d_model * 2 * n_io + tokens * mc.n_heads * 4 * 2 if n_io else None
-                roof["traffic_detail"] = {"fetch": round(tr["fetch"]), "write": round(tr["write"]),
-                                          "launches": tr["launches"],
-                                          **{kind: {"bytes_per_launch": round(tr[kind]["bytes"]),
-                                                    "launches": tr[kind]["launches"],
-                                                    **({"x_algorithmic": round(tr[kind]["bytes"] / alg, 2)}
-                                                       if alg else {})}
-                                             for kind in ("global", "local") if kind in tr},
-                                          **({"algorithmic_bytes_per_launch": alg} if alg else {}),
-                                          "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-                                                    "one micro-step; FETCH_SIZE x2 (gfx950)"}
+                roof["traffic_detail"] = traffic_detail(dom, tr, tokens, mc)
+        # the other attention kernels' traffic, same passes
+        if traffic:
+            roof["traffic_by_kernel"] = {k: traffic_detail(k, tr, tokens, mc) for k, tr in traffic.items() if tr}
         if rank == 0:
             log("[bench] per-kernel time in one micro-step (ms):")
             for k, (n, ms_, fl_) in kernels[:40]:

@@ -38,9 +38,26 @@
 #define AS3 __attribute__((address_space(3)))
 
 // timing-only experiment builds (tools/build_variant.sh -DOWLK_FUSED_EXP=n; results are WRONG):
-// bit 0: no hand-off (no flag polls, no sum loads); bit 1: no dQ products / stores either
+// bit 0: no hand-off (no flag polls, no sum loads); bit 1: no dQ products / stores either;
+// bit 2: no dS image writes
 #ifndef OWLK_FUSED_EXP
 #define OWLK_FUSED_EXP 0
+#endif
+// dQ^T products: 0 = 16x16x32 MFMAs on all 8 waves (one 16-d x 32-q quarter each); 1 = 32x32x16
+// MFMAs on waves 0-3 (one 32 x 32 tile each; one transposed LDS read per 16K FLOP instead of
+// three), waves 4-7 go straight on to the next tile
+#ifndef OWLK_FUSED_DQ32
+#define OWLK_FUSED_DQ32 1
+#endif
+// 1: the dQ products of the previous tile run in four parts between this tile's MFMA groups
+// (before each softmax-gradient VALU block and after each dK/dV group); 0: all at the top of the step
+// timing-only statistics build: workspace int32 words 10 / 11 count the hand-offs that found the
+// flag down at mid-step (blocking poll at the next step's top) / all hand-offs, per wave
+#ifndef OWLK_FUSED_STATS
+#define OWLK_FUSED_STATS 0
+#endif
+#ifndef OWLK_FUSED_DQ_SPLIT
+#define OWLK_FUSED_DQ_SPLIT 0
 #endif
 
 namespace {
@@ -58,7 +75,7 @@ constexpr int FLAGL_OFF = ACC_OFF + 8 * 2048;    // per wave 256 B: a polled fla
 constexpr int MISC_OFF = FLAGL_OFF + 8 * 256;
 constexpr int SMEM_BYTES = MISC_OFF + 16;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
-constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word
+constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
 
 struct FusedP {
@@ -86,6 +103,17 @@ DEV unsigned xcc_id() {
 
 // per-lane byte offset of frag_tr16(lds, row0, ds, lane) for any row0 that is a multiple of 16
 // (swz_dual repeats every 16 rows); the second ds_read_b64_tr_b16 of the fragment is 2 KiB further
+// per-lane byte offsets of frag_tr<SW_DUAL>(lds, row0, 0, cb, lane) (32x32x16 fragment of column
+// group cb) for any row0 that is a multiple of 16: its two ds_read_b64_tr_b16 (rows 4 h + qq and
+// 8 + 4 h + qq); the swizzle repeats every 16 rows
+DEV void tr32_lane_off(int cb, int lane, int& oa, int& ob) {
+  const int g = lane >> 4, h = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int ra = 4 * h + qq, rb = ra + 8;
+  const int ch = 4 * cb + 2 * (g & 1) + (pp >> 1);
+  oa = ra * 128 + ((ch ^ swz_dual(ra)) << 4) + 8 * (pp & 1);
+  ob = rb * 128 + ((ch ^ swz_dual(rb)) << 4) + 8 * (pp & 1);
+}
+
 DEV int tr16_lane_off(int ds, int lane) {
   const int c = lane & 15, g = lane >> 4;
   const int x = 4 * g + (c >> 2);
@@ -102,22 +130,27 @@ DEV int tr16_lane_off(int ds, int lane) {
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 DEV unsigned lds_addr(const void* p) { return (unsigned)(uintptr_t)(const AS3 void*)p; }
-// one 16-B-per-lane LDS-DMA wave-instruction to the wave-uniform LDS byte address `lds`
-DEV void dma16(unsigned lds, const void* src) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+// one LDS-DMA wave-instruction (16 or 4 B per lane) to the wave-uniform LDS byte address `lds`
+// from the wave-uniform base `base` (SGPRs) + a 32-bit per-lane byte offset, so no 64-bit per-lane
+// address is kept live across the sweep.  No instruction offset: it would move the LDS
+// destination too (M0 + offset + lane * size)
+DEV void dma16(unsigned lds, const void* base, unsigned off) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(off), "s"(base)
+               : "memory", "m0");
 }
-DEV void dma4(unsigned lds, const void* src) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+DEV void dma4(unsigned lds, const void* base, unsigned off) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2" ::"s"(lds), "v"(off), "s"(base)
+               : "memory", "m0");
 }
 // the hand-off's loads (sc1: past this CU's L1, cdna_hip_programming.md Guideline 16) land in LDS
 // too: a register destination of an asm load whose wait is a separate statement could be copied
 // by the compiler before the data arrives; these are read back by ds_read after vm_wait
-DEV void dma16_sc1(unsigned lds, const void* src) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1" ::"s"(lds), "v"(src)
+DEV void dma16_sc1(unsigned lds, const void* base, unsigned off) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 sc1" ::"s"(lds), "v"(off), "s"(base)
                : "memory", "m0");
 }
-DEV void dma4_sc1(unsigned lds, const void* src) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1" ::"s"(lds), "v"(src)
+DEV void dma4_sc1(unsigned lds, const void* base, unsigned off) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2 sc1" ::"s"(lds), "v"(off), "s"(base)
                : "memory", "m0");
 }
 #pragma clang diagnostic pop
@@ -170,9 +203,21 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const int L = p.L;
   char* kimg = smem + KIMG_OFF;
   // this wave's quarter of dQ^T: d tile dt, query tiles qt0, qt0 + 1 (16 rows / columns each)
+  // (DQ32: waves 0-3, d tile of 32 dt32 x query tile of 32 qt32)
+  constexpr int DQ32 = OWLK_FUSED_DQ32;
+  constexpr int NACC = DQ32 ? 4 : 2;  // f32x4 registers of this wave's part of a tile's sum
+  static_assert(DQ32 == 0 || DQ32 == 1, "OWLK_FUSED_DQ32: 0 or 1");
+  // does this wave form (and hand off) its part of tile i's dQ?
+  auto dq_wave = [&](int) { return DQ32 == 0 || w < 4; };
+  const int wq = w;  // this wave's part of a tile's sum / its landing zone
   const int dt = w & 3, qt0 = 2 * (w >> 2);
-  const unsigned acc_lane = (unsigned)((2 * w) * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
+  const int dt32 = w & 1, qt32 = (w >> 1) & 1;
+  const unsigned acc_lane = (unsigned)(wq * NACC * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
   const int offk = tr16_lane_off(dt, lane), offs0 = tr16_lane_off(qt0, lane), offs1 = tr16_lane_off(qt0 + 1, lane);
+  int ok32a, ok32b, os32a, os32b;
+  tr32_lane_off(dt32, lane, ok32a, ok32b);
+  tr32_lane_off(qt32, lane, os32a, os32b);
+  if (blockIdx.x == 0 && threadIdx.x == 0) p.hdr[9] = FKB;  // for readers of the workspace (tests)
 
   // per-lane LDS-DMA source offsets of a 64-row tile (wave w: rows 8 w .. 8 w + 7, one 1-KiB
   // wave-instruction, swizzled source chunk)
@@ -226,24 +271,24 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const int ch = (lane & 7) ^ swz_dual(row);
       int gr = k0 + row;
       gr = gr < L ? gr : L - 1;
-      dma16(lds_addr(kimg + (32 * w + 8 * i) * 128), K + (long)gr * p.ldk + ch * 8);
+      dma16(lds_addr(kimg + (32 * w + 8 * i) * 128), K + (long)k0 * p.ldk, (unsigned)(((gr - k0) * p.ldk + ch * 8) * 2));
     }
     // ring: Q and dO 64-row tiles + the lse2 / delta rows (waves 0 / 1)
     auto issue = [&](int t) {
       char* buf = smem + (t & 1) * RING_SLOT;
       const int q0 = t * FQT;
       if (q0 + FQT <= L) {
-        dma16(lds_addr(buf + 8 * w * 128), (const char*)(Q + (long)q0 * p.ldq) + offq);
-        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), (const char*)(dO + (long)q0 * p.ldo) + offd);
+        dma16(lds_addr(buf + 8 * w * 128), Q + (long)q0 * p.ldq, offq);
+        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)q0 * p.ldo, offd);
       } else {
         int gr = q0 + drow;
         gr = gr < L ? gr : L - 1;
-        dma16(lds_addr(buf + 8 * w * 128), Q + (long)gr * p.ldq + dch * 8);
-        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)gr * p.ldo + dch * 8);
+        dma16(lds_addr(buf + 8 * w * 128), Q + (long)q0 * p.ldq, (unsigned)(((gr - q0) * p.ldq + dch * 8) * 2));
+        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)q0 * p.ldo, (unsigned)(((gr - q0) * p.ldo + dch * 8) * 2));
       }
       if (w < 2) {
-        const int src = q0 + lane < L ? q0 + lane : L - 1;
-        dma4(lds_addr(buf + 2 * TILE_BYTES + w * FQT * 4), (w ? DLT : LSE) + src);
+        const int src = q0 + lane < L ? lane : L - 1 - q0;
+        dma4(lds_addr(buf + 2 * TILE_BYTES + w * FQT * 4), (w ? DLT : LSE) + q0, (unsigned)(src * 4));
       }
     };
 
@@ -289,22 +334,36 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 
     // store a finished dQ^T quarter of tile i: bf16 dQ by the tile's last contributor, else the fp32
     // sum (sc1 write-through; plain in the local variant)
-    auto store_dq = [&](int i, const f32x4 (&vals)[2]) {
+    auto store_dq = [&](int i, const f32x4 (&vals)[NACC]) {
       const bool last = j >= tile_jhi(p, i);
       if (last && !counting) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int qrow = i * FQT + 16 * (qt0 + e) + c;
+        if constexpr (DQ32 != 0) {  // lane: query 32 qt32 + (lane & 31); register 4 rr + e: d 32 dt32 + 8 rr + 4 h + e
+          const int qrow = i * FQT + 32 * qt32 + (lane & 31);
           if (qrow < L) {
-            bf16x4 o4;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o4[r] = (bf16)(vals[e][r] * -p.scale);  // dS accumulated negated
-            *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 16 * dt + 4 * g) = o4;
+            for (int rr = 0; rr < 4; ++rr) {
+              bf16x4 o4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o4[r] = (bf16)(vals[rr][r] * -p.scale);  // dS accumulated negated
+              *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 32 * dt32 + 8 * rr + 4 * (lane >> 5)) =
+                  o4;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int qrow = i * FQT + 16 * (qt0 + e) + c;
+            if (qrow < L) {
+              bf16x4 o4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o4[r] = (bf16)(vals[e][r] * -p.scale);  // dS accumulated negated
+              *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 16 * dt + 4 * g) = o4;
+            }
           }
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
+        for (int e = 0; e < NACC; ++e) {
           const int off = (int)(i * ACC_TILE_BYTES + acc_lane + e * 1024);
           if constexpr (local)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vals[e]), ars, off, 0, 0);
@@ -313,38 +372,65 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         }
       }
     };
-    const char* accp = p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES + acc_lane;
-    char* accl = smem + ACC_OFF + w * 2048;  // this wave's landing zone (lane-linear, as acc_lane)
+    const char* accp = p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES;  // + acc_lane per lane
+    char* accl = smem + ACC_OFF + wq * NACC * 1024;  // this wave's landing zone (lane-linear, as acc_lane)
     char* flagl = smem + FLAGL_OFF + w * 256;
     auto load_acc = [&](int i) {  // -> accl, read back by read_acc after vm_wait
-      dma16_sc1(lds_addr(accl), accp + (long)i * ACC_TILE_BYTES);
-      dma16_sc1(lds_addr(accl + 1024), accp + (long)i * ACC_TILE_BYTES + 1024);
+#pragma unroll
+      for (int e = 0; e < NACC; ++e) dma16_sc1(lds_addr(accl + e * 1024), accp + (long)i * ACC_TILE_BYTES + e * 1024, acc_lane);
     };
-    auto read_acc = [&](f32x4 (&vals)[2]) {
-      vals[0] = *(const f32x4*)(accl + lane * 16);
-      vals[1] = *(const f32x4*)(accl + 1024 + lane * 16);
+    auto read_acc = [&](f32x4 (&vals)[NACC]) {
+#pragma unroll
+      for (int e = 0; e < NACC; ++e) vals[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
     };
-    // dQ^T quarter of tile i from its dS image (written in the step of tile i) over the 256 keys.
-    // frag_tr16 at row0 = 32 kk: the swizzle repeats every 16 rows, so one per-lane offset per
-    // 16-column group and immediate offsets kk * 4 KiB (+ 2 KiB for the second 4-row group)
-    auto dq_mfma = [&](int i, f32x4 (&a)[2]) {
+
+    // dQ^T of tile i from its dS image (written in the step of tile i) over the item's keys, in
+    // NPART parts (part p: keys FKB p / NPART ..), so the parts can sit between the next tile's
+    // MFMA groups.  Accumulators: qacc (32x32x16 form) or qa (16x16x32 form).
+    // 16x16x32 form: frag_tr16 at row0 = 32 kk; the swizzle repeats every 16 rows, so one per-lane
+    // offset per 16-column group and immediate offsets kk * 4 KiB (+ 2 KiB for the second 4-row group)
+    constexpr int NPART = 4;
+    f32x16 qacc;
+    f32x4 qa[2];
+    auto dq_part = [&](int i, int part) {
       if constexpr (counting) {
+        if (part == 0) {
+          if constexpr (DQ32 != 0) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
+            for (int e = 0; e < 16; ++e) qacc[e] += 1.f;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) a[e][r] += 1.f;
+            for (int e = 0; e < 2; ++e)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) qa[e][r] += 1.f;
+          }
+        }
         return;
       }
-      const char* kb = kimg + offk;
-      const char* sb0 = smem + DS_OFF + (i & 1) * DS_BYTES + offs0;
-      const char* sb1 = smem + DS_OFF + (i & 1) * DS_BYTES + offs1;
+      if constexpr (DQ32 != 0) {
+        // dQ^T[32 d x 32 q] += K^T[32 d x 16 keys] dS^T[16 keys x 32 q]; both fragments by frag_tr's
+        // permuted row order (the same for A and B)
+        const char* dsb = smem + DS_OFF + (i & 1) * DS_BYTES;
 #pragma unroll
-      for (int kk = 0; kk < FKB / 32; ++kk) {
-        const bf16x8 ak = join_tr(ds_read_tr16(kb + 4096 * kk), ds_read_tr16(kb + 4096 * kk + 2048));
-        const bf16x8 b0 = join_tr(ds_read_tr16(sb0 + 4096 * kk), ds_read_tr16(sb0 + 4096 * kk + 2048));
-        const bf16x8 b1 = join_tr(ds_read_tr16(sb1 + 4096 * kk), ds_read_tr16(sb1 + 4096 * kk + 2048));
-        a[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b0, a[0], 0, 0, 0);
-        a[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b1, a[1], 0, 0, 0);
+        for (int k2 = 0; k2 < FKB / 16 / NPART; ++k2) {
+          const int kk = part * (FKB / 16 / NPART) + k2;
+          const bf16x8 ak = join_tr(ds_read_tr16(kimg + ok32a + 2048 * kk), ds_read_tr16(kimg + ok32b + 2048 * kk));
+          const bf16x8 bs = join_tr(ds_read_tr16(dsb + os32a + 2048 * kk), ds_read_tr16(dsb + os32b + 2048 * kk));
+          qacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ak, bs, qacc, 0, 0, 0);
+        }
+      } else {
+        const char* kb = kimg + offk;
+        const char* sb0 = smem + DS_OFF + (i & 1) * DS_BYTES + offs0;
+        const char* sb1 = smem + DS_OFF + (i & 1) * DS_BYTES + offs1;
+#pragma unroll
+        for (int k2 = 0; k2 < FKB / 32 / NPART; ++k2) {
+          const int kk = part * (FKB / 32 / NPART) + k2;
+          const bf16x8 ak = join_tr(ds_read_tr16(kb + 4096 * kk), ds_read_tr16(kb + 4096 * kk + 2048));
+          const bf16x8 b0 = join_tr(ds_read_tr16(sb0 + 4096 * kk), ds_read_tr16(sb0 + 4096 * kk + 2048));
+          const bf16x8 b1 = join_tr(ds_read_tr16(sb1 + 4096 * kk), ds_read_tr16(sb1 + 4096 * kk + 2048));
+          qa[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b0, qa[0], 0, 0, 0);
+          qa[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b1, qa[1], 0, 0, 0);
+        }
       }
     };
 
@@ -358,28 +444,69 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     // the predecessor's sum of the tile whose dQ is formed next lands in accl: loaded in the
     // tile's own step (after its first half, once the flag polled at the top has had time to
     // arrive), read back at the top of the next step; the chain's first block starts from zeros
+    // pend: the predecessor's sum of the tile whose dQ is formed next, read from the landing zone
+    // at the end of the tile's own step
     bool ready = true;
-    auto dq_tile = [&](int i) {  // form, add and store dQ^T of tile i
-      if (OWLK_FUSED_EXP & 2) return;
-      f32x4 a[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 pend[NACC];
+    // the chain's sum so far of tile i into the accumulators (zeros for the chain's first block)
+    auto dq_begin = [&](int i) {
+      f32x4 a[NACC];
+#pragma unroll
+      for (int e = 0; e < NACC; ++e) a[e] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (j > 0 && !(OWLK_FUSED_EXP & 1)) {
-        if (!ready) {
+        if (OWLK_FUSED_STATS && lane == 0) {
+          __hip_atomic_fetch_add(p.hdr + 11, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ready) {
+#pragma unroll
+          for (int e = 0; e < NACC; ++e) a[e] = pend[e];
+        } else {
+          // the flag was not up at mid-step: poll, then load the sum now (its own landing zone;
+          // nothing else of this wave's is in flight at the top of a step)
           wait_flag(flg + i * FLAG_STRIDE, j, p.hdr + 8);
           load_acc(i);
+          vm_wait<0>();
+          read_acc(a);
         }
-        vm_wait<0>();  // the accumulator loads are the only vector-memory ops in flight
-        read_acc(a);
       }
-      dq_mfma(i, a);
+      if constexpr (DQ32 != 0) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qacc[4 * rr + r] = a[rr][r];
+      } else {
+        qa[0] = a[0];
+        qa[1] = a[1];
+      }
+    };
+    auto dq_end = [&](int i) {
+      f32x4 a[NACC];
+      if constexpr (DQ32 != 0) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[rr][r] = qacc[4 * rr + r];
+      } else {
+        a[0] = qa[0];
+        a[1] = qa[1];
+      }
       store_dq(i, a);
     };
     for (int t = t_hi; t >= t_lo; --t) {
       const int q0 = t * FQT;
-      // top: dQ of tile t + 1 from its dS image (step t + 1), stored at once; this step's barrier
-      // drains the stores, then the flag goes out
-      if (t + 1 <= t_hi) dq_tile(t + 1);
-      // in issue order: dQ stores, the flag poll, the ring's LDS-DMA of tile t - 1
-      if (j > 0 && !(OWLK_FUSED_EXP & 1)) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE);
+      // dQ of tile t + 1 from its dS image (step t + 1) in NPART parts between this step's MFMA
+      // groups (or all at the top), stored at the end of the step; the step's barrier drains the
+      // stores, then the flag goes out
+      const bool dq_on = !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi && dq_wave(t + 1);
+      if (dq_on) {
+        dq_begin(t + 1);
+        if (!OWLK_FUSED_DQ_SPLIT)
+#pragma unroll
+          for (int part = 0; part < NPART; ++part) dq_part(t + 1, part);
+      }
+      // in issue order: the flag poll, the ring's LDS-DMA of tile t - 1
+      if (j > 0 && dq_wave(t) && !(OWLK_FUSED_EXP & 1)) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
       const bool dma = t - 1 >= t_lo;
       if (dma) issue(t - 1);
 
@@ -419,6 +546,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
               *(bf16x4*)(dsw + r * 128 + ((ch ^ swz_dual(r)) << 4) + 8 * (g & 1)) = bf16x4{};
             }
           }
+          if (OWLK_FUSED_DQ_SPLIT && dq_on) dq_part(t + 1, 2 * qb);
         } else {
           f32x4 st[2][2], dp[2][2];  // [16-row query tile][key tile]
 #pragma unroll
@@ -441,6 +569,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
                 dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vf[t2][ks], dp[qs][t2], 0, 0, 0);
               }
             }
+          // a dQ part runs in the matrix pipe while this wave does the softmax-gradient VALU work
+          if (OWLK_FUSED_DQ_SPLIT && dq_on) dq_part(t + 1, 2 * qb);
 #pragma unroll
           for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
@@ -477,8 +607,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
             const bf16x4 lo4 = __builtin_shufflevector(sf[t2], sf[t2], 0, 1, 2, 3);
             const bf16x4 hi4 = __builtin_shufflevector(sf[t2], sf[t2], 4, 5, 6, 7);
             const int ch0 = 4 * qb + (g >> 1), ch1 = ch0 + 2;
-            *(bf16x4*)(dsw + r * 128 + ((ch0 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = lo4;
-            *(bf16x4*)(dsw + r * 128 + ((ch1 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = hi4;
+            if (!(OWLK_FUSED_EXP & 4)) {
+              *(bf16x4*)(dsw + r * 128 + ((ch0 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = lo4;
+              *(bf16x4*)(dsw + r * 128 + ((ch1 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = hi4;
+            }
           }
 #pragma unroll
           for (int ds = 0; ds < 4; ++ds) {
@@ -491,8 +623,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
             }
           }
         }
+        if (OWLK_FUSED_DQ_SPLIT && dq_on) dq_part(t + 1, 2 * qb + 1);
         if (qb == 0) {
-          if (j > 0 && !(OWLK_FUSED_EXP & 1)) {  // the flag polled at the top has had half a tile to arrive
+          if (j > 0 && dq_wave(t) && !(OWLK_FUSED_EXP & 1)) {  // the flag polled at the top has had half a tile to arrive
             if (!dma)
               vm_wait<0>();
             else if (w < 2)
@@ -507,19 +640,22 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           }
         }
       }
-      // every wave: its dQ(t + 1) stores and the ring's tile t - 1 have landed (vmcnt counts in
-      // issue order; the accumulator loads of tile t, issued last, may stay in flight)
-      if (loads_out)
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (dq_on) dq_end(t + 1);
+      // every wave: its dQ(t + 1) stores, the ring's tile t - 1 and its sum of tile t have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (loads_out) read_acc(pend);
       __syncthreads();
       if (t + 1 <= t_hi && threadIdx.x == 0)
         __hip_atomic_store(flg + (t + 1) * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
-    dq_tile(t_lo);
+    if (!(OWLK_FUSED_EXP & 2) && dq_wave(t_lo)) {
+      dq_begin(t_lo);
+#pragma unroll
+      for (int part = 0; part < NPART; ++part) dq_part(t_lo, part);
+      dq_end(t_lo);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
     if (threadIdx.x == 0)
@@ -556,6 +692,19 @@ int fused_grid(int dev) {
     cached[dev] = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
   }
   return cached[dev];
+}
+
+// the XCD-local hand-off needs a workgroup on every one of the 8 per-XCD queues' XCDs (an XCC id
+// no workgroup reports would leave its queue undrained): only on a device of 8 XCCs (SPX mode;
+// workgroups reach the XCCs round-robin)
+bool all_xcds_present(int dev) {
+  static int cached[64] = {};  // 0 unknown, 1 yes, -1 no
+  if (dev < 0 || dev >= 64) return false;
+  if (!cached[dev]) {
+    int n = 0;
+    cached[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) == hipSuccess && n == 8 ? 1 : -1;
+  }
+  return cached[dev] > 0;
 }
 
 }  // namespace
@@ -619,6 +768,8 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   int dev = 0;
   (void)hipGetDevice(&dev);
   const dim3 grid((unsigned)fused_grid(dev));
+  // the XCD-local hand-off only on an 8-XCC device (else: write-through)
+  if ((variant & 1) && !all_xcds_present(dev)) variant &= ~1;
   switch (variant & 3) {
     case 0: hipLaunchKernelGGL((attn_bwd_fused_k<false, false>), grid, dim3(512), 0, s, p); break;
     case 1: hipLaunchKernelGGL((attn_bwd_fused_k<true, false>), grid, dim3(512), 0, s, p); break;

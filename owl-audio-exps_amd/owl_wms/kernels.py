@@ -432,9 +432,10 @@ def _bwd_side_stream(device, D, mask):
 def fused_bwd_variant(D, mask):
     """owlk_attn_bwd_fused variant for this layer, or None for the two-kernel backward.  The single
     pass serves head_dim 64 with an unwindowed, document-free mask (dit_v4's global layers);
-    OWLK_BWD_FUSED = 0 turns it off, 1 (default) takes the write-through hand-off, 2 keeps each
-    chain's dQ sums in one XCD's L2 (include/owlk.h)."""
-    env = os.environ.get("OWLK_BWD_FUSED", "1")
+    OWLK_BWD_FUSED = 0 turns it off, 1 takes the write-through hand-off, 2 (default) keeps each
+    chain's dQ sums in one XCD's L2 (the library runs it write-through on a device without 8 XCCs;
+    include/owlk.h)."""
+    env = os.environ.get("OWLK_BWD_FUSED", "2")
     if env == "0" or D != 64 or mask.window is not None or mask.arrays is not None or mask.q_offset != 0:
         return None
     return 1 if env == "2" else 0

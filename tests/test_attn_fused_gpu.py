@@ -14,7 +14,7 @@ from oracle import ref_ops as R
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-FKB, FQT = 256, 64  # keys per work item, query rows per tile (attn_bwd_fused.hip)
+FQT = 64  # query rows per swept tile (attn_bwd_fused.hip); keys per work item: workspace int32 word 9
 
 
 def K():
@@ -57,7 +57,7 @@ def _hdr(ws):
     return ws[:256].view(torch.int32).cpu()
 
 
-def _jhi(L, tpf, causal):
+def _jhi(L, tpf, causal, FKB):
     """last key block each 64-row query tile sees (frame-causal, unwindowed)"""
     nkb = (L + FKB - 1) // FKB
     out = []
@@ -156,7 +156,9 @@ def test_attention_bwd_fused_handoff_counts(shape, variant):
     torch.cuda.synchronize()
     assert _hdr(ws)[8].item() == 0, "hand-off wait timed out"
     nchain, nt = B * H, (L + FQT - 1) // FQT
-    want = (_jhi(L, tpf, causal) + 1).to(DEV)
+    fkb = _hdr(ws)[9].item()
+    assert fkb in (128, 256)
+    want = (_jhi(L, tpf, causal, fkb) + 1).to(DEV)
     flags = ws[256:256 + nchain * nt * 64].view(torch.int32).view(nchain, nt, 16)[:, :, 0]
     assert torch.equal(flags, want[None, :].to(torch.int32).expand(nchain, nt))
     acc = ws[256 + nchain * nt * 64:256 + nchain * nt * (64 + FQT * 64 * 4)].view(torch.float32)

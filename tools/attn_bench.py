@@ -110,7 +110,11 @@ def main():
                 for var in (0, 1):
                     t_fu[var].append(timeit(lambda: K.attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv,
                                                                      D ** -0.5, var, ws), args.iters))
-            err = ws[:256].view(torch.int32)[8].item()
+            hw = ws[:256].view(torch.int32).cpu()
+            err = hw[8].item()
+            if hw[11].item():  # OWLK_FUSED_STATS builds: the last call's (xcd-local) hand-offs
+                print(f"  fused hand-offs (last call): {hw[10].item()} of {hw[11].item()} found the flag down at "
+                      f"mid-step ({hw[10].item() / hw[11].item():.3f})", flush=True)
             for var, nm in ((0, "write-through"), (1, "xcd-local")):
                 t = min(t_fu[var])
                 print(f"  fused {t:8.3f} ms  {8 * D * pairs / t / 1e9:7.1f} TF/s alg (8 D pairs; 10 D executed: "
