@@ -32,6 +32,8 @@
 // Forward progress: items are dequeued in increasing key-block order per chain from per-XCD atomic
 // queues; an item waits only on its chain predecessor, which a running workgroup dequeued earlier.
 // Spins are bounded by the real-time clock (error word in the workspace header).
+#include <utility>
+
 #include "attn_common.hpp"
 
 #define AS1 __attribute__((address_space(1)))
@@ -43,21 +45,19 @@
 #ifndef OWLK_FUSED_EXP
 #define OWLK_FUSED_EXP 0
 #endif
-// dQ^T products: 0 = 16x16x32 MFMAs on all 8 waves (one 16-d x 32-q quarter each); 1 = 32x32x16
-// MFMAs on waves 0-3 (one 32 x 32 tile each; one transposed LDS read per 16K FLOP instead of
-// three), waves 4-7 go straight on to the next tile
-#ifndef OWLK_FUSED_DQ32
-#define OWLK_FUSED_DQ32 1
-#endif
-// 1: the dQ products of the previous tile run in four parts between this tile's MFMA groups
-// (before each softmax-gradient VALU block and after each dK/dV group); 0: all at the top of the step
 // timing-only statistics build: workspace int32 words 10 / 11 count the hand-offs that found the
 // flag down at mid-step (blocking poll at the next step's top) / all hand-offs, per wave
 #ifndef OWLK_FUSED_STATS
 #define OWLK_FUSED_STATS 0
 #endif
-#ifndef OWLK_FUSED_DQ_SPLIT
-#define OWLK_FUSED_DQ_SPLIT 0
+// timing-only profile build: per-phase shader-clock cycles of the sweep, summed over waves, as uint64
+// at workspace bytes 128.. : [dQ waves | other waves] x {dQ part, main, end-of-step vmcnt, barrier}
+#ifndef OWLK_FUSED_PROF
+#define OWLK_FUSED_PROF 0
+#endif
+// software-pipeline depth of the 32x32 dQ products (k-steps of reads in flight ahead of the MFMA)
+#ifndef OWLK_FUSED_DQ_PF
+#define OWLK_FUSED_DQ_PF 2
 #endif
 
 namespace {
@@ -77,6 +77,7 @@ constexpr int SMEM_BYTES = MISC_OFF + 16;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
 constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
+constexpr int NACC = 4;                        // 16-B words per lane of a wave's 32 x 32 part of a tile's sum
 
 struct FusedP {
   const bf16 *q, *k, *v, *dout;
@@ -114,11 +115,17 @@ DEV void tr32_lane_off(int cb, int lane, int& oa, int& ob) {
   ob = rb * 128 + ((ch ^ swz_dual(rb)) << 4) + 8 * (pp & 1);
 }
 
-DEV int tr16_lane_off(int ds, int lane) {
+// per-lane byte offset of frag_row16(lds, row0, ks, lane) for any row0 that is a multiple of 16
+DEV unsigned row16_lane_off(int ks, int lane) {
+  const int r = lane & 15;
+  return (unsigned)(r * 128 + (((4 * ks + (lane >> 4)) ^ swz_dual(r)) << 4));
+}
+
+DEV unsigned tr16_lane_off(int ds, int lane) {
   const int c = lane & 15, g = lane >> 4;
   const int x = 4 * g + (c >> 2);
   const int ch = 2 * ds + ((c & 3) >> 1);
-  return x * 128 + ((ch ^ swz_dual(x)) << 4) + 8 * (c & 1);
+  return (unsigned)(x * 128 + ((ch ^ swz_dual(x)) << 4) + 8 * (c & 1));
 }
 
 // Every vector-memory access of the sweep goes through inline asm, and the waits are counted by
@@ -157,6 +164,40 @@ DEV void dma4_sc1(unsigned lds, const void* base, unsigned off) {
 template <int N>
 DEV void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Every LDS read of the sweep's MFMA operands is inline asm, software-pipelined by hand (left to
+// itself hipcc reads each MFMA's operands right before it into one register set and waits
+// lgkmcnt(0)); retired by lgkm2 / lgkm4, whose "+v" operands keep every consumer below the wait.
+// LDS operations complete in order and the sweep has no scalar loads, so a count N waits for all
+// but the N youngest LDS operations: counting only the asm reads issued after the awaited ones is
+// exact or over-waits (compiler-issued LDS stores / reads in between only add younger operations)
+template <int OFF>
+DEV s16x4 tr_rd(unsigned lds) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lds), "n"(OFF) : "memory");
+  return r;
+}
+template <int OFF, typename T>
+DEV T rd128(unsigned lds) {
+  T r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(lds), "n"(OFF) : "memory");
+  return r;
+}
+template <int N, typename A, typename B>
+DEV void lgkm2(A& a, B& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+template <int N, typename A, typename B, typename C, typename D>
+DEV void lgkm4(A& a, B& b, C& c, D& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
+}
+template <typename F, int... I>
+DEV void static_for_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+DEV void static_for(F&& f) {
+  static_for_(f, std::make_integer_sequence<int, N>{});
 }
 
 DEV int frame(const FusedP& p, int idx) { return p.magic ? (int)__umulhi((unsigned)idx, p.magic) : idx; }
@@ -202,21 +243,18 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const unsigned xcc = xcc_id();
   const int L = p.L;
   char* kimg = smem + KIMG_OFF;
-  // this wave's quarter of dQ^T: d tile dt, query tiles qt0, qt0 + 1 (16 rows / columns each)
-  // (DQ32: waves 0-3, d tile of 32 dt32 x query tile of 32 qt32)
-  constexpr int DQ32 = OWLK_FUSED_DQ32;
-  constexpr int NACC = DQ32 ? 4 : 2;  // f32x4 registers of this wave's part of a tile's sum
-  static_assert(DQ32 == 0 || DQ32 == 1, "OWLK_FUSED_DQ32: 0 or 1");
-  // does this wave form (and hand off) its part of tile i's dQ?
-  auto dq_wave = [&](int) { return DQ32 == 0 || w < 4; };
-  const int wq = w;  // this wave's part of a tile's sum / its landing zone
-  const int dt = w & 3, qt0 = 2 * (w >> 2);
+  // dQ^T of a tile: waves 0-3, one 32 x 32 tile each (d tile dt32, query tile qt32)
+  const bool dq_wave = w < 4;
   const int dt32 = w & 1, qt32 = (w >> 1) & 1;
-  const unsigned acc_lane = (unsigned)(wq * NACC * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
-  const int offk = tr16_lane_off(dt, lane), offs0 = tr16_lane_off(qt0, lane), offs1 = tr16_lane_off(qt0 + 1, lane);
+  const unsigned acc_lane = (unsigned)(w * NACC * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
   int ok32a, ok32b, os32a, os32b;
   tr32_lane_off(dt32, lane, ok32a, ok32b);
   tr32_lane_off(qt32, lane, os32a, os32b);
+  // per-lane LDS byte offsets in a ring slot (row0 a multiple of 16 in the immediate): frag_row16
+  // of k-step 0 / 1, frag_tr16 of column group ds, the lse2 / delta rows of lane group g
+  const unsigned ro0 = row16_lane_off(0, lane), ro1 = row16_lane_off(1, lane);
+  const unsigned tro0 = tr16_lane_off(0, lane), tro1 = tr16_lane_off(1, lane), tro2 = tr16_lane_off(2, lane),
+                 tro3 = tr16_lane_off(3, lane);
   if (blockIdx.x == 0 && threadIdx.x == 0) p.hdr[9] = FKB;  // for readers of the workspace (tests)
 
   // per-lane LDS-DMA source offsets of a 64-row tile (wave w: rows 8 w .. 8 w + 7, one 1-KiB
@@ -225,6 +263,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const int dch = (lane & 7) ^ swz_dual(drow);
   const unsigned offq = (unsigned)((drow * p.ldq + dch * 8) * 2), offd = (unsigned)((drow * p.ldo + dch * 8) * 2);
 
+  unsigned long long prof[4] = {0ull, 0ull, 0ull, 0ull};
   for (;;) {
     // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local)
     if (threadIdx.x == 0) {
@@ -247,7 +286,14 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     __syncthreads();
     const int chain = __builtin_amdgcn_readfirstlane(sh_item[0]);
     const int j = __builtin_amdgcn_readfirstlane(sh_item[1]);
-    if (chain < 0) return;
+    if (chain < 0) {
+      if (OWLK_FUSED_PROF && lane == 0) {
+        unsigned long long* pp = (unsigned long long*)((char*)p.hdr + 128) + (w < 4 ? 0 : 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) __hip_atomic_fetch_add(pp + e, prof[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
 
     const int b = chain / p.H;
     const int head = chain % p.H;
@@ -332,123 +378,83 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) dk[ds][t2] = dv[ds][t2] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // store a finished dQ^T quarter of tile i: bf16 dQ by the tile's last contributor, else the fp32
-    // sum (sc1 write-through; plain in the local variant)
-    auto store_dq = [&](int i, const f32x4 (&vals)[NACC]) {
+    // a finished dQ^T tile of this wave: bf16 dQ by the tile's last contributor (lane: query
+    // 32 qt32 + (lane & 31); register 4 rr + e: d 32 dt32 + 8 rr + 4 h + e), else the fp32 sum
+    // (sc1 write-through; plain in the local variant)
+    f32x16 qacc;
+    auto store_dq = [&](int i) {
       const bool last = j >= tile_jhi(p, i);
       if (last && !counting) {
-        if constexpr (DQ32 != 0) {  // lane: query 32 qt32 + (lane & 31); register 4 rr + e: d 32 dt32 + 8 rr + 4 h + e
-          const int qrow = i * FQT + 32 * qt32 + (lane & 31);
-          if (qrow < L) {
+        const int qrow = i * FQT + 32 * qt32 + (lane & 31);
+        if (qrow < L) {
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              bf16x4 o4;
+          for (int rr = 0; rr < 4; ++rr) {
+            bf16x4 o4;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) o4[r] = (bf16)(vals[rr][r] * -p.scale);  // dS accumulated negated
-              *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 32 * dt32 + 8 * rr + 4 * (lane >> 5)) =
-                  o4;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int qrow = i * FQT + 16 * (qt0 + e) + c;
-            if (qrow < L) {
-              bf16x4 o4;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) o4[r] = (bf16)(vals[e][r] * -p.scale);  // dS accumulated negated
-              *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 16 * dt + 4 * g) = o4;
-            }
+            for (int r = 0; r < 4; ++r) o4[r] = (bf16)(qacc[4 * rr + r] * -p.scale);  // dS accumulated negated
+            *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 32 * dt32 + 8 * rr + 4 * (lane >> 5)) = o4;
           }
         }
       } else {
 #pragma unroll
         for (int e = 0; e < NACC; ++e) {
           const int off = (int)(i * ACC_TILE_BYTES + acc_lane + e * 1024);
+          const f32x4 v4 = {qacc[4 * e], qacc[4 * e + 1], qacc[4 * e + 2], qacc[4 * e + 3]};
           if constexpr (local)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vals[e]), ars, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), ars, off, 0, 0);
           else
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vals[e]), ars, off, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), ars, off, 0, 16);
         }
       }
     };
     const char* accp = p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES;  // + acc_lane per lane
-    char* accl = smem + ACC_OFF + wq * NACC * 1024;  // this wave's landing zone (lane-linear, as acc_lane)
+    char* accl = smem + ACC_OFF + w * NACC * 1024;  // this wave's landing zone (lane-linear, as acc_lane)
     char* flagl = smem + FLAGL_OFF + w * 256;
-    auto load_acc = [&](int i) {  // -> accl, read back by read_acc after vm_wait
+    auto load_acc = [&](int i) {  // -> accl, read back after vm_wait
 #pragma unroll
       for (int e = 0; e < NACC; ++e) dma16_sc1(lds_addr(accl + e * 1024), accp + (long)i * ACC_TILE_BYTES + e * 1024, acc_lane);
     };
-    auto read_acc = [&](f32x4 (&vals)[NACC]) {
-#pragma unroll
-      for (int e = 0; e < NACC; ++e) vals[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
-    };
 
-    // dQ^T of tile i from its dS image (written in the step of tile i) over the item's keys, in
-    // NPART parts (part p: keys FKB p / NPART ..), so the parts can sit between the next tile's
-    // MFMA groups.  Accumulators: qacc (32x32x16 form) or qa (16x16x32 form).
-    // 16x16x32 form: frag_tr16 at row0 = 32 kk; the swizzle repeats every 16 rows, so one per-lane
-    // offset per 16-column group and immediate offsets kk * 4 KiB (+ 2 KiB for the second 4-row group)
-    constexpr int NPART = 4;
-    f32x16 qacc;
-    f32x4 qa[2];
-    auto dq_part = [&](int i, int part) {
+    // dQ^T[32 d x 32 q] of tile i += K^T[32 d x 16 keys] dS^T[16 keys x 32 q] over the item's keys,
+    // from the K image and the tile's dS image (written in the tile's own step); both fragments in
+    // frag_tr's permuted row order (the same for A and B), software-pipelined OWLK_FUSED_DQ_PF
+    // k-steps deep
+    auto dq_mfma = [&](int i) {
       if constexpr (counting) {
-        if (part == 0) {
-          if constexpr (DQ32 != 0) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) qacc[e] += 1.f;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) qa[e][r] += 1.f;
-          }
-        }
+        for (int e = 0; e < 16; ++e) qacc[e] += 1.f;
         return;
       }
-      if constexpr (DQ32 != 0) {
-        // dQ^T[32 d x 32 q] += K^T[32 d x 16 keys] dS^T[16 keys x 32 q]; both fragments by frag_tr's
-        // permuted row order (the same for A and B)
-        const char* dsb = smem + DS_OFF + (i & 1) * DS_BYTES;
-#pragma unroll
-        for (int k2 = 0; k2 < FKB / 16 / NPART; ++k2) {
-          const int kk = part * (FKB / 16 / NPART) + k2;
-          const bf16x8 ak = join_tr(ds_read_tr16(kimg + ok32a + 2048 * kk), ds_read_tr16(kimg + ok32b + 2048 * kk));
-          const bf16x8 bs = join_tr(ds_read_tr16(dsb + os32a + 2048 * kk), ds_read_tr16(dsb + os32b + 2048 * kk));
-          qacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ak, bs, qacc, 0, 0, 0);
-        }
-      } else {
-        const char* kb = kimg + offk;
-        const char* sb0 = smem + DS_OFF + (i & 1) * DS_BYTES + offs0;
-        const char* sb1 = smem + DS_OFF + (i & 1) * DS_BYTES + offs1;
-#pragma unroll
-        for (int k2 = 0; k2 < FKB / 32 / NPART; ++k2) {
-          const int kk = part * (FKB / 32 / NPART) + k2;
-          const bf16x8 ak = join_tr(ds_read_tr16(kb + 4096 * kk), ds_read_tr16(kb + 4096 * kk + 2048));
-          const bf16x8 b0 = join_tr(ds_read_tr16(sb0 + 4096 * kk), ds_read_tr16(sb0 + 4096 * kk + 2048));
-          const bf16x8 b1 = join_tr(ds_read_tr16(sb1 + 4096 * kk), ds_read_tr16(sb1 + 4096 * kk + 2048));
-          qa[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b0, qa[0], 0, 0, 0);
-          qa[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, b1, qa[1], 0, 0, 0);
-        }
-      }
+      constexpr int NK = FKB / 16, PF = OWLK_FUSED_DQ_PF;
+      const unsigned kb0 = lds_addr(kimg), sb0 = lds_addr(smem + DS_OFF + (i & 1) * DS_BYTES);
+      const unsigned ka = kb0 + ok32a, kb = kb0 + ok32b, sa = sb0 + os32a, sb = sb0 + os32b;
+      s16x4 r[PF + 1][4];
+      auto rd = [&](auto kc) {
+        constexpr int k2 = decltype(kc)::value, sl = k2 % (PF + 1);
+        r[sl][0] = tr_rd<2048 * k2>(ka);
+        r[sl][1] = tr_rd<2048 * k2>(kb);
+        r[sl][2] = tr_rd<2048 * k2>(sa);
+        r[sl][3] = tr_rd<2048 * k2>(sb);
+      };
+      static_for<PF>(rd);
+      static_for<NK>([&](auto kc) {
+        constexpr int k2 = decltype(kc)::value, sl = k2 % (PF + 1);
+        if constexpr (k2 + PF < NK) rd(std::integral_constant<int, k2 + PF>{});
+        constexpr int younger = 4 * (PF < NK - 1 - k2 ? PF : NK - 1 - k2);
+        lgkm4<younger>(r[sl][0], r[sl][1], r[sl][2], r[sl][3]);
+        qacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(join_tr(r[sl][0], r[sl][1]), join_tr(r[sl][2], r[sl][3]), qacc,
+                                                       0, 0, 0);
+      });
     };
 
     issue(t_hi);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // dqc: the predecessor's sum of tile t, loaded in step t (after the first half of the tile, once
-    // the flag polled at the top has had time to arrive), the initial value of dQ(t)'s MFMA chain at
-    // the top of step t - 1; zeros for the chain's first block
-    // the predecessor's sum of the tile whose dQ is formed next lands in accl: loaded in the
-    // tile's own step (after its first half, once the flag polled at the top has had time to
-    // arrive), read back at the top of the next step; the chain's first block starts from zeros
-    // pend: the predecessor's sum of the tile whose dQ is formed next, read from the landing zone
-    // at the end of the tile's own step
+    // ready: the predecessor's sum of the tile whose dQ is formed next was found published at
+    // mid-step of the tile's own step and is in flight to this wave's landing zone (waited for at
+    // the top of the next step); else it is polled and loaded there.  Zeros for the chain's first block
     bool ready = true;
-    f32x4 pend[NACC];
-    // the chain's sum so far of tile i into the accumulators (zeros for the chain's first block)
     auto dq_begin = [&](int i) {
       f32x4 a[NACC];
 #pragma unroll
@@ -458,64 +464,26 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           __hip_atomic_fetch_add(p.hdr + 11, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (ready) {
-#pragma unroll
-          for (int e = 0; e < NACC; ++e) a[e] = pend[e];
-        } else {
-          // the flag was not up at mid-step: poll, then load the sum now (its own landing zone;
-          // nothing else of this wave's is in flight at the top of a step)
+        if (!ready) {
           wait_flag(flg + i * FLAG_STRIDE, j, p.hdr + 8);
           load_acc(i);
-          vm_wait<0>();
-          read_acc(a);
         }
-      }
-      if constexpr (DQ32 != 0) {
+        vm_wait<0>();  // the sum's loads are this wave's only vector-memory ops in flight here
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) qacc[4 * rr + r] = a[rr][r];
-      } else {
-        qa[0] = a[0];
-        qa[1] = a[1];
+        for (int e = 0; e < NACC; ++e) a[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
       }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qacc[4 * rr + r] = a[rr][r];
     };
-    auto dq_end = [&](int i) {
-      f32x4 a[NACC];
-      if constexpr (DQ32 != 0) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) a[rr][r] = qacc[4 * rr + r];
-      } else {
-        a[0] = qa[0];
-        a[1] = qa[1];
-      }
-      store_dq(i, a);
-    };
+
     for (int t = t_hi; t >= t_lo; --t) {
       const int q0 = t * FQT;
-      // dQ of tile t + 1 from its dS image (step t + 1) in NPART parts between this step's MFMA
-      // groups (or all at the top), stored at the end of the step; the step's barrier drains the
-      // stores, then the flag goes out
-      const bool dq_on = !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi && dq_wave(t + 1);
-      if (dq_on) {
-        dq_begin(t + 1);
-        if (!OWLK_FUSED_DQ_SPLIT)
-#pragma unroll
-          for (int part = 0; part < NPART; ++part) dq_part(t + 1, part);
-      }
-      // in issue order: the flag poll, the ring's LDS-DMA of tile t - 1
-      if (j > 0 && dq_wave(t) && !(OWLK_FUSED_EXP & 1)) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
-      const bool dma = t - 1 >= t_lo;
-      if (dma) issue(t - 1);
-
-      const char* tb = smem + (t & 1) * RING_SLOT;
-      const char* lq = tb;
-      const char* ld = tb + TILE_BYTES;
-      const float* l2 = (const float*)(tb + 2 * TILE_BYTES);
-      const float* dlt = l2 + FQT;
-      char* dsw = smem + DS_OFF + (t & 1) * DS_BYTES;
+      const unsigned long long c0 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+      const bool dq_on = !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi && dq_wave;
+      // the predecessor's sum of tile t + 1 (waits for this wave's vector memory: before any DMA)
+      if (dq_on) dq_begin(t + 1);
 
       int kind = TILE_FULL;
       if (t < full_lo || t >= full_hi) {
@@ -524,6 +492,46 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       }
       kind = __builtin_amdgcn_readfirstlane(kind);
       const bool masked = kind == TILE_PARTIAL;
+
+      // a tile's S / dP operands of query rows 32 qb .. + 31 (lse2, delta rows, Q and dO
+      // fragments), by asm in the order they are consumed: 12 LDS reads
+      const unsigned sbase = lds_addr(smem + (t & 1) * RING_SLOT);
+      const unsigned a_r0 = sbase + ro0, a_r1 = sbase + ro1, a_l = sbase + 16 * g;
+      f32x4 lr[2], dr[2];
+      bf16x8 aq[2][2], ad[2][2];  // [k step][16-row query tile]
+      auto issue_a = [&](auto qbc) {
+        constexpr int qb = decltype(qbc)::value;
+        static_for<2>([&](auto qsc) {
+          constexpr int qs = decltype(qsc)::value, row = 32 * qb + 16 * qs;
+          lr[qs] = rd128<2 * TILE_BYTES + 4 * row, f32x4>(a_l);
+          dr[qs] = rd128<2 * TILE_BYTES + 4 * FQT + 4 * row, f32x4>(a_l);
+        });
+        static_for<2>([&](auto qsc) {
+          constexpr int qs = decltype(qsc)::value, row = 32 * qb + 16 * qs;
+          aq[0][qs] = rd128<128 * row, bf16x8>(a_r0);
+          ad[0][qs] = rd128<TILE_BYTES + 128 * row, bf16x8>(a_r0);
+        });
+        static_for<2>([&](auto qsc) {
+          constexpr int qs = decltype(qsc)::value, row = 32 * qb + 16 * qs;
+          aq[1][qs] = rd128<128 * row, bf16x8>(a_r1);
+          ad[1][qs] = rd128<TILE_BYTES + 128 * row, bf16x8>(a_r1);
+        });
+      };
+
+      // dQ of tile t + 1 from its dS image (step t + 1), stored at once; this step's barrier drains
+      // the stores, then the flag goes out
+      if (dq_on) {
+        dq_mfma(t + 1);
+        store_dq(t + 1);
+      }
+      // in issue order: the dQ stores, the ring's LDS-DMA of tile t - 1, the flag poll
+      const unsigned long long c1 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+      const bool dma = t - 1 >= t_lo;
+      if (dma) issue(t - 1);
+      const bool poll = j > 0 && dq_wave && !(OWLK_FUSED_EXP & 1);
+      if (poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
+
+      char* dsw = smem + DS_OFF + (t & 1) * DS_BYTES;
       unsigned long long bh[2] = {0ull, 0ull};
       if (masked) {  // query rows [frame(key) tpf, L) (causal) / [0, L) of the tile, per key
 #pragma unroll
@@ -533,8 +541,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         }
       }
       bool loads_out = false;
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
+      static_for<2>([&](auto qbc) {
+        constexpr int qb = decltype(qbc)::value;
         if (kind == TILE_EMPTY) {
           // no allowed pair for this wave's keys: its rows of the dS image are zero
 #pragma unroll
@@ -546,31 +554,44 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
               *(bf16x4*)(dsw + r * 128 + ((ch ^ swz_dual(r)) << 4) + 8 * (g & 1)) = bf16x4{};
             }
           }
-          if (OWLK_FUSED_DQ_SPLIT && dq_on) dq_part(t + 1, 2 * qb);
         } else {
+          // S / dP (12 reads in flight, oldest first: lse2 / delta rows, then k step 0, 1).  Issued
+          // here, not earlier: holding them across the step's control flow overflows the 256-VGPR
+          // budget (tried: 100-200 VGPRs spilled)
+          issue_a(qbc);
           f32x4 st[2][2], dp[2][2];  // [16-row query tile][key tile]
+          lgkm4<8>(lr[0], dr[0], lr[1], dr[1]);
 #pragma unroll
           for (int qs = 0; qs < 2; ++qs) {
-            const int rowb = 32 * qb + 16 * qs + 4 * g;
-            const f32x4 Lr = *(const f32x4*)(l2 + rowb);
-            const f32x4 Dr = *(const f32x4*)(dlt + rowb);
-            st[qs][0] = st[qs][1] = Lr;
-            dp[qs][0] = dp[qs][1] = Dr;
+            st[qs][0] = st[qs][1] = lr[qs];
+            dp[qs][0] = dp[qs][1] = dr[qs];
           }
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int qs = 0; qs < 2; ++qs) {
-              const bf16x8 aq = frag_row16(lq, 32 * qb + 16 * qs, ks, lane);
-              const bf16x8 ad = frag_row16(ld, 32 * qb + 16 * qs, ks, lane);
+          static_for<2>([&](auto ksc) {
+            constexpr int ks = decltype(ksc)::value;
+            static_for<2>([&](auto qsc) {
+              constexpr int qs = decltype(qsc)::value;
+              lgkm2<6 - 4 * ks - 2 * qs>(aq[ks][qs], ad[ks][qs]);
 #pragma unroll
               for (int t2 = 0; t2 < 2; ++t2) {
-                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kf[t2][ks], st[qs][t2], 0, 0, 0);
-                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vf[t2][ks], dp[qs][t2], 0, 0, 0);
+                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks][qs], kf[t2][ks], st[qs][t2], 0, 0, 0);
+                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[ks][qs], vf[t2][ks], dp[qs][t2], 0, 0, 0);
               }
-            }
-          // a dQ part runs in the matrix pipe while this wave does the softmax-gradient VALU work
-          if (OWLK_FUSED_DQ_SPLIT && dq_on) dq_part(t + 1, 2 * qb);
+            });
+          });
+          // the dV / dK operands (dO^T, Q^T of these 32 rows): 16 reads, landing under the
+          // softmax-gradient VALU work below
+          s16x4 tq[4][4];  // [column group ds][dO^T lo, hi, Q^T lo, hi]
+          auto rd_t = [&](auto dsc, unsigned a) {
+            constexpr int ds = decltype(dsc)::value;
+            tq[ds][0] = tr_rd<TILE_BYTES + 128 * 32 * qb>(a);
+            tq[ds][1] = tr_rd<TILE_BYTES + 128 * 32 * qb + 2048>(a);
+            tq[ds][2] = tr_rd<128 * 32 * qb>(a);
+            tq[ds][3] = tr_rd<128 * 32 * qb + 2048>(a);
+          };
+          rd_t(std::integral_constant<int, 0>{}, sbase + tro0);
+          rd_t(std::integral_constant<int, 1>{}, sbase + tro1);
+          rd_t(std::integral_constant<int, 2>{}, sbase + tro2);
+          rd_t(std::integral_constant<int, 3>{}, sbase + tro3);
 #pragma unroll
           for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
@@ -580,13 +601,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           if (masked) {
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2) {
-              if (qb == 0) {
-                apply_bits4<0>(st[0][t2], bh[t2], 0.f);
-                apply_bits4<16>(st[1][t2], bh[t2], 0.f);
-              } else {
-                apply_bits4<32>(st[0][t2], bh[t2], 0.f);
-                apply_bits4<48>(st[1][t2], bh[t2], 0.f);
-              }
+              apply_bits4<32 * qb>(st[0][t2], bh[t2], 0.f);
+              apply_bits4<32 * qb + 16>(st[1][t2], bh[t2], 0.f);
             }
           }
           bf16x8 pf[2], sf[2];
@@ -612,26 +628,22 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
               *(bf16x4*)(dsw + r * 128 + ((ch1 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = hi4;
             }
           }
-#pragma unroll
-          for (int ds = 0; ds < 4; ++ds) {
-            const bf16x8 ado = frag_tr16(ld, 32 * qb, ds, lane);
-            const bf16x8 aqt = frag_tr16(lq, 32 * qb, ds, lane);
+          // dV / dK (the dS stores above are younger than every read waited for: the counts
+          // only over-wait)
+          static_for<4>([&](auto dsc) {
+            constexpr int ds = decltype(dsc)::value;
+            lgkm4<4 * (3 - ds)>(tq[ds][0], tq[ds][1], tq[ds][2], tq[ds][3]);
+            const bf16x8 ado = join_tr(tq[ds][0], tq[ds][1]), aqt = join_tr(tq[ds][2], tq[ds][3]);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2) {
               dv[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pf[t2], dv[ds][t2], 0, 0, 0);
               dk[ds][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aqt, sf[t2], dk[ds][t2], 0, 0, 0);
             }
-          }
+          });
         }
-        if (OWLK_FUSED_DQ_SPLIT && dq_on) dq_part(t + 1, 2 * qb + 1);
-        if (qb == 0) {
-          if (j > 0 && dq_wave(t) && !(OWLK_FUSED_EXP & 1)) {  // the flag polled at the top has had half a tile to arrive
-            if (!dma)
-              vm_wait<0>();
-            else if (w < 2)
-              vm_wait<3>();  // Q, dO and an lse2 / delta row
-            else
-              vm_wait<2>();
+        if constexpr (qb == 0) {
+          if (poll) {  // the flag polled at the top has had half a tile to arrive
+            vm_wait<0>();  // the dQ stores, the ring's DMA and the flag poll, in issue order
             ready = __builtin_amdgcn_readfirstlane(*(const int*)(flagl + lane * 4)) >= j;
             if (ready) {
               load_acc(t);
@@ -639,24 +651,34 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
             }
           }
         }
-      }
-      if (dq_on) dq_end(t + 1);
-      // every wave: its dQ(t + 1) stores, the ring's tile t - 1 and its sum of tile t have landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (loads_out) read_acc(pend);
+      });
+      // every wave: its dQ(t + 1) stores and the ring's tile t - 1 have landed (vmcnt counts in
+      // issue order; the sum's loads of tile t, issued last, stay in flight to the next step's top)
+      const unsigned long long c2 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+      if (loads_out)
+        vm_wait<NACC>();
+      else
+        vm_wait<0>();
+      const unsigned long long c3 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       __syncthreads();
+      if (OWLK_FUSED_PROF) {
+        const unsigned long long c4 = __builtin_amdgcn_s_memtime();
+        prof[0] += c1 - c0;
+        prof[1] += c2 - c1;
+        prof[2] += c3 - c2;
+        prof[3] += c4 - c3;
+      }
       if (t + 1 <= t_hi && threadIdx.x == 0)
         __hip_atomic_store(flg + (t + 1) * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
-    if (!(OWLK_FUSED_EXP & 2) && dq_wave(t_lo)) {
+    if (!(OWLK_FUSED_EXP & 2) && dq_wave) {
       dq_begin(t_lo);
-#pragma unroll
-      for (int part = 0; part < NPART; ++part) dq_part(t_lo, part);
-      dq_end(t_lo);
+      dq_mfma(t_lo);
+      store_dq(t_lo);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait<0>();
     __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
     if (threadIdx.x == 0)
       __hip_atomic_store(flg + t_lo * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
