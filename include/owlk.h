@@ -191,7 +191,9 @@ int owlk_attn_bwd_dq(const void* q, long ldq, long sqb, const void* k, long ldk,
  * 256-B aligned; the entry zeroes its header / flags itself (one memset on the stream).  variant:
  * 0 = write-through (sc1) sums, any workgroup placement; bit 0 = a chain's sums kept in one XCD's
  * L2 (plain stores, per-XCD queues; taken only on a device of 8 XCCs, hipDeviceAttributeNumberOfXccs,
- * else the call runs write-through); bit 1 = test mode: every contributor adds 1.0
+ * else the call runs write-through); bits 2-5 = chains of an XCD queue swept at a time (0 = all of
+ * them interleaved; 1 gives each chain every workgroup of its XCD, so its sums and Q / dO tiles are
+ * re-read fewer times); bit 1 = test mode: every contributor adds 1.0
  * instead of its dQ part and the last one keeps the fp32 sum in ws (dQ not written).  After the
  * call, ws int32 word 8 != 0 means a hand-off wait timed out (never expected). */
 long owlk_attn_bwd_fused_ws_bytes(long B, int H, long L, int head_dim);

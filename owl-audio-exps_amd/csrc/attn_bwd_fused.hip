@@ -94,6 +94,7 @@ struct FusedP {
   int* flags;  // [nchain][ntiles] x FLAG_STRIDE
   char* acc;   // [nchain][ntiles][ACC_TILE_BYTES]
   int variant;
+  int group;  // chains of a queue taken at a time (>= 1)
 };
 
 DEV unsigned xcc_id() {
@@ -276,8 +277,14 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         if (__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) continue;
         const int n = __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n < total) {
-          chain = x + 8 * (n % cx);
-          jj = n / cx;
+          // the queue's chains in groups of p.group (j-major inside a group): fewer chains at a
+          // time give each chain more workgroups, so a key block's successor follows closer behind
+          // and the chain's sums and Q / dO tiles are re-read fewer times (each generation of
+          // concurrent blocks re-sweeps the chain)
+          const int gfull = p.group * p.nkb, gi = n / gfull, m = n - gi * gfull;
+          const int gsz = cx - gi * p.group < p.group ? cx - gi * p.group : p.group;
+          chain = x + 8 * (gi * p.group + m % gsz);
+          jj = m / gsz;
         }
       }
       sh_item[0] = chain;
@@ -783,6 +790,7 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   p.flags = (int*)((char*)ws + HDR_BYTES);
   p.acc = (char*)ws + HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4;
   p.variant = variant;
+  p.group = (variant >> 2) & 15 ? (variant >> 2) & 15 : 1 << 20;  // variant bits 2-5; 0 = all of the queue's chains
   hipStream_t s = (hipStream_t)stream;
   // counters, error word and flags are zero on entry (one memset node, 16-B multiple from the start)
   if (hipMemsetAsync(ws, 0, (size_t)(HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4), s) != hipSuccess)

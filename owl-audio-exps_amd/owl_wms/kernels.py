@@ -438,7 +438,11 @@ def fused_bwd_variant(D, mask):
     env = os.environ.get("OWLK_BWD_FUSED", "2")
     if env == "0" or D != 64 or mask.window is not None or mask.arrays is not None or mask.q_offset != 0:
         return None
-    return 1 if env == "2" else 0
+    # OWLK_BWD_FUSED_GROUP: chains of an XCD queue swept at a time (variant bits 2-5; 0 = all);
+    # one at a time (default) gives each chain the XCD's 32 workgroups: -2 % time and -54 % HBM
+    # traffic against all three of dit_v4's at once (profiles/r4j_ab.log)
+    group = int(os.environ.get("OWLK_BWD_FUSED_GROUP", "1"))
+    return (1 if env == "2" else 0) | (group & 15) << 2
 
 
 def attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, variant=0, ws=None):

@@ -105,17 +105,28 @@ def main():
             # single-pass backward (owlk_attn_bwd_fused): both hand-off forms, interleaved
             nb = _lib.lib().owlk_attn_bwd_fused_ws_bytes(1, H, L, D)
             ws = torch.empty(nb, device="cuda", dtype=torch.uint8)
-            t_fu = {0: [], 1: []}
+            fvars = [int(x) for x in os.environ.get("FUSED_VARIANTS", "0,1").split(",")]
+            t_fu = {v: [] for v in fvars}
             for _ in range(2):
-                for var in (0, 1):
+                for var in fvars:
                     t_fu[var].append(timeit(lambda: K.attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv,
                                                                      D ** -0.5, var, ws), args.iters))
             hw = ws[:256].view(torch.int32).cpu()
             err = hw[8].item()
+            pw = ws[128:192].view(torch.int64).cpu().tolist()
+            if any(pw):  # OWLK_FUSED_PROF builds: cycles per phase, dQ waves | other waves
+                tot = sum(pw[:4]) or 1
+                tot2 = sum(pw[4:]) or 1
+                print("  fused phases (s_memtime cycles, share of the sweep): dQ waves: " +
+                      ", ".join(f"{n} {v / tot:.3f}" for n, v in zip(("dq", "main", "vmwait", "barrier"), pw[:4])) +
+                      " | other waves: " +
+                      ", ".join(f"{n} {v / tot2:.3f}" for n, v in zip(("dq", "main", "vmwait", "barrier"), pw[4:])) +
+                      f" | cycles per wave-step {tot / 1:.3e} total", flush=True)
             if hw[11].item():  # OWLK_FUSED_STATS builds: the last call's (xcd-local) hand-offs
                 print(f"  fused hand-offs (last call): {hw[10].item()} of {hw[11].item()} found the flag down at "
                       f"mid-step ({hw[10].item() / hw[11].item():.3f})", flush=True)
-            for var, nm in ((0, "write-through"), (1, "xcd-local")):
+            for var in fvars:
+                nm = ("xcd-local" if var & 1 else "write-through") + (f" group {var >> 2}" if var >> 2 else "")
                 t = min(t_fu[var])
                 print(f"  fused {t:8.3f} ms  {8 * D * pairs / t / 1e9:7.1f} TF/s alg (8 D pairs; 10 D executed: "
                       f"{10 * D * pairs / t / 1e9:.1f}) [{nm}: {t_fu[var]}] timeout word {err}", flush=True)
