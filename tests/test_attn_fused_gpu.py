@@ -82,7 +82,7 @@ FUSED_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 5])  # write-through, XCD-local, XCD-local one chain at a time
 @pytest.mark.parametrize("case", FUSED_CASES)
 def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
     k = K()
@@ -113,8 +113,8 @@ def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
 @pytest.mark.parametrize("case", [(2, 8, 48, 64, True), (1, 2, 40, 64, False), (1, 1, 300, 1, True)])
 def test_attention_bwd_fused_deterministic(case):
     """Every query tile receives its key blocks' dQ parts in key-block order, so two runs -- and the
-    write-through and the XCD-local hand-offs, which differ only in where the sums live -- give the
-    same bits."""
+    write-through and the XCD-local hand-offs, which differ only in where the sums live, and the
+    chain-group dequeue orders (variant bits 2-5) -- give the same bits."""
     k = K()
     B, H, nf, tpf, causal = case
     D, L = 64, nf * tpf
@@ -123,7 +123,7 @@ def test_attention_bwd_fused_deterministic(case):
     o, lse = k.attn_fwd(q, kk, v, H, D, mask)
     delta = _delta(o, do, H, D)
     runs = []
-    for variant in (0, 0, 1, 1):
+    for variant in (0, 0, 1, 1, 5, 9):
         g = [torch.full_like(q, float("nan")) for _ in range(3)]
         ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *g, D ** -0.5, variant)
         torch.cuda.synchronize()
@@ -134,7 +134,7 @@ def test_attention_bwd_fused_deterministic(case):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [2, 3, 7])
 @pytest.mark.parametrize("shape", [(1, 24, 1536, 64, True), (2, 3, 20, 64, True), (1, 1, 300, 1, True),
                                    (1, 2, 40, 64, False), (1, 8, 96, 65, True)])
 def test_attention_bwd_fused_handoff_counts(shape, variant):
