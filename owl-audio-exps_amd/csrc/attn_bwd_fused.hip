@@ -1,4 +1,5 @@
-// Frame-masked flash attention backward in ONE pass (gfx950, head_dim 64, unwindowed masks).
+// Frame-masked flash attention backward in ONE pass (gfx950, head_dim 64, causal / windowed frame masks
+// without documents).
 //
 // Reference: the single compiled flex_attention backward behind attn.py:13-16, 106-109 (torch's
 // flex template forms dQ, dK and dV in one kernel).  Same math as attn_bwd.hip:
@@ -87,7 +88,8 @@ struct FusedP {
   long sqb, skb, svb, sob, sdqb, sdkb, sdvb;  // batch strides
   int L;                                      // Lq == Lkv
   int H, nchain, ntiles, nkb;
-  int tpf, causal;    // the mask: frame = token / tpf; causal or none (no window, no documents)
+  int tpf, causal;    // the mask: frame = token / tpf; causal or not, window (frames; <= 0: none); no documents
+  int window;
   unsigned magic;     // floor(2^32 / tpf) + 1 (exact frame division below 2^32 / tpf); 0 if tpf == 1
   float scale, scale_log2;
   int* hdr;    // dequeue counters / error word
@@ -203,14 +205,41 @@ DEV void static_for(F&& f) {
 
 DEV int frame(const FusedP& p, int idx) { return p.magic ? (int)__umulhi((unsigned)idx, p.magic) : idx; }
 
-// last key block that query tile i sees (the mask is causal-by-frame or empty); every block
-// 0 .. jhi(i) sweeps tile i, each exactly once
+// The frame mask without documents (attn.py:24-62): query frame fq sees key frame fk iff fk <= fq
+// (causal) and |fq - fk| < window (window > 0).  Key frame fk is seen by query tokens
+// [q_lo_frame(fk) tpf, q_hi_end(fk)).
+DEV int q_lo_frame(const FusedP& p, int fk) {
+  return p.causal ? fk : (p.window > 0 && fk - p.window + 1 > 0 ? fk - p.window + 1 : 0);
+}
+DEV long q_hi_end(const FusedP& p, int fk) {
+  if (p.window <= 0) return p.L;
+  const long e = (long)(fk + p.window) * p.tpf;
+  return e < p.L ? e : p.L;
+}
+// key block j sweeps query tiles sweep_lo(j) .. sweep_hi(j), both non-decreasing in j, so the
+// blocks that sweep tile i are the contiguous range tile_jlo(i) .. tile_jhi(i): the closed forms
+// of min{j : sweep_hi(j) >= i} and max{j : sweep_lo(j) <= i} (tests/test_attn_fused_gpu.py checks
+// them against those definitions, and the counting mode checks the kernel's hand-offs against them)
+DEV int sweep_lo(const FusedP& p, int j) { return (int)((long)q_lo_frame(p, frame(p, j * FKB)) * p.tpf / FQT); }
+DEV int sweep_hi(const FusedP& p, int j) {
+  const int k1 = j * FKB + FKB - 1 < p.L ? j * FKB + FKB - 1 : p.L - 1;
+  return (int)((q_hi_end(p, frame(p, k1)) - 1) / FQT);
+}
+DEV int tile_jlo(const FusedP& p, int i) {
+  if (p.window <= 0) return 0;
+  const long x = (long)(frame(p, i * FQT) - p.window + 1) * p.tpf;
+  return x > 0 ? (int)(x / FKB) : 0;
+}
 DEV int tile_jhi(const FusedP& p, int i) {
-  if (!p.causal) return p.nkb - 1;
   const int ql = i * FQT + FQT - 1 < p.L ? i * FQT + FQT - 1 : p.L - 1;
-  const long kend = (long)(frame(p, ql) + 1) * p.tpf;
-  const int ke = kend < p.L ? (int)kend : p.L;
-  const int j = (ke - 1) / FKB;
+  long f = frame(p, ql);
+  if (!p.causal) {
+    if (p.window <= 0) return p.nkb - 1;
+    f += p.window - 1;
+  }
+  const long kend = (f + 1) * p.tpf;
+  const long ke = kend < p.L ? kend : p.L;
+  const int j = (int)((ke - 1) / FKB);
   return j < p.nkb - 1 ? j : p.nkb - 1;
 }
 
@@ -314,8 +343,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
         p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES, (short)0, p.ntiles * ACC_TILE_BYTES, 0x00020000);
     const int k0 = j * FKB, kw0 = k0 + 32 * w;
-    const int t_hi = p.ntiles - 1;
-    const int t_lo = p.causal ? (int)(((long)frame(p, k0) * p.tpf) / FQT) : 0;
+    const int t_hi = sweep_hi(p, j);
+    const int t_lo = sweep_lo(p, j);
 
     // ---- K image of the item (unscaled K: the dQ^T A operand), 4 wave-instructions per wave
 #pragma unroll
@@ -368,13 +397,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         vf[t2][ks] = pack8(h8);
       }
     }
-    // tile classes of this wave's 32 keys (frames wfk0 .. wfk1): FULL from the first query tile
-    // whose first frame is >= wfk1 (causal) up to the last whole tile, PARTIAL / EMPTY by frames
-    // outside that range
+    // tile classes of this wave's 32 keys (frames wfk0 .. wfk1): FULL on the whole tiles every one
+    // of its keys sees entirely (rows from q_lo_frame(wfk1) tpf to q_hi_end(wfk0)), EMPTY on tiles
+    // none of them sees, else PARTIAL
     const bool wave_live = kw0 < L;
     const int wfk0 = frame(p, kw0), wfk1 = frame(p, kw0 + 31 < L ? kw0 + 31 : L - 1);
-    int full_lo = p.causal ? (int)(((long)wfk1 * p.tpf + FQT - 1) / FQT) : 0;
-    int full_hi = L / FQT;  // exclusive: whole tiles only
+    const long seen_lo = (long)q_lo_frame(p, wfk0) * p.tpf, seen_hi = q_hi_end(p, wfk1);  // any key
+    int full_lo = (int)(((long)q_lo_frame(p, wfk1) * p.tpf + FQT - 1) / FQT);
+    int full_hi = (int)(q_hi_end(p, wfk0) / FQT);  // exclusive: whole tiles only
+    if (full_hi > L / FQT) full_hi = L / FQT;
     if (!wave_live || kw0 + 32 > L) full_lo = full_hi = 0;
     full_lo = __builtin_amdgcn_readfirstlane(full_lo);
     full_hi = __builtin_amdgcn_readfirstlane(full_hi);
@@ -466,7 +497,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       f32x4 a[NACC];
 #pragma unroll
       for (int e = 0; e < NACC; ++e) a[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (j > 0 && !(OWLK_FUSED_EXP & 1)) {
+      if (j > tile_jlo(p, i) && !(OWLK_FUSED_EXP & 1)) {
         if (OWLK_FUSED_STATS && lane == 0) {
           __hip_atomic_fetch_add(p.hdr + 11, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -494,8 +525,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 
       int kind = TILE_FULL;
       if (t < full_lo || t >= full_hi) {
-        const int fq1 = frame(p, q0 + FQT - 1 < L ? q0 + FQT - 1 : L - 1);
-        kind = !wave_live || (p.causal && wfk0 > fq1) ? TILE_EMPTY : TILE_PARTIAL;
+        const long r1 = q0 + FQT < L ? q0 + FQT : L;
+        kind = !wave_live || r1 <= seen_lo || q0 >= seen_hi ? TILE_EMPTY : TILE_PARTIAL;
       }
       kind = __builtin_amdgcn_readfirstlane(kind);
       const bool masked = kind == TILE_PARTIAL;
@@ -535,7 +566,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const unsigned long long c1 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dma = t - 1 >= t_lo;
       if (dma) issue(t - 1);
-      const bool poll = j > 0 && dq_wave && !(OWLK_FUSED_EXP & 1);
+      const bool poll = j > tile_jlo(p, t) && dq_wave && !(OWLK_FUSED_EXP & 1);
       if (poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
 
       char* dsw = smem + DS_OFF + (t & 1) * DS_BYTES;
@@ -543,8 +574,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       if (masked) {  // query rows [frame(key) tpf, L) (causal) / [0, L) of the tile, per key
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2) {
-          const long lo = p.causal ? (long)frame(p, my_k[t2]) * p.tpf : 0;
-          bh[t2] = my_k[t2] < L ? range_bits(lo - q0, (long)L - q0) >> (4 * g) : 0ull;
+          const int fk = frame(p, my_k[t2]);
+          const long lo = (long)q_lo_frame(p, fk) * p.tpf, hi = q_hi_end(p, fk);
+          bh[t2] = my_k[t2] < L ? range_bits(lo - q0, hi - q0) >> (4 * g) : 0ull;
         }
       }
       bool loads_out = false;
@@ -758,8 +790,7 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   OWLK_REQUIRE(ldq < (1L << 31) && ldk < (1L << 31) && ldv < (1L << 31) && ldo < (1L << 31) && lddq < (1L << 31) &&
                    lddk < (1L << 31) && lddv < (1L << 31),
                "attn_bwd_fused: row strides too large");
-  OWLK_REQUIRE(window <= 0 && !kv_lo && !q_hi && !run_start && !doc,
-               "attn_bwd_fused: unwindowed, document-free masks only");
+  OWLK_REQUIRE(!kv_lo && !q_hi && !run_start && !doc, "attn_bwd_fused: document-free masks only");
   OWLK_REQUIRE(L < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_bwd_fused: sequence too long");
   OWLK_REQUIRE(fused_tiles(L) * (long)ACC_TILE_BYTES < (1L << 31), "attn_bwd_fused: sequence too long");
   OWLK_REQUIRE(B * H < (1L << 24), "attn_bwd_fused: too many heads");
@@ -783,6 +814,7 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   p.nkb = (int)((L + FKB - 1) / FKB);
   p.tpf = (int)tpf;
   p.causal = causal ? 1 : 0;
+  p.window = window > 0 ? window : 0;
   p.magic = tpf > 1 ? (unsigned)((1ull << 32) / (unsigned long long)tpf + 1) : 0u;
   p.scale = scale;
   p.scale_log2 = scale * 1.4426950408889634f;

@@ -57,28 +57,43 @@ def _hdr(ws):
     return ws[:256].view(torch.int32).cpu()
 
 
-def _jhi(L, tpf, causal, FKB):
-    """last key block each 64-row query tile sees (frame-causal, unwindowed)"""
-    nkb = (L + FKB - 1) // FKB
+def _sweeps(L, tpf, causal, window, FKB):
+    """query tiles each key block sweeps (attn_bwd_fused.hip sweep_lo / sweep_hi): from the first
+    query tile that sees its first key's frame to the last that sees its last key's frame"""
     out = []
+    for j in range((L + FKB - 1) // FKB):
+        f0, f1 = (j * FKB) // tpf, min(j * FKB + FKB - 1, L - 1) // tpf
+        qlo = f0 if causal else (max(0, f0 - window + 1) if window else 0)
+        qend = min(L, (f1 + window) * tpf) if window else L
+        out.append(((qlo * tpf) // FQT, (qend - 1) // FQT))
+    return out
+
+
+def _jrange(L, tpf, causal, window, FKB):
+    """the key blocks that sweep each query tile, by the definition (min / max over the sweeps),
+    independent of the kernel's closed forms tile_jlo / tile_jhi"""
+    sw = _sweeps(L, tpf, causal, window, FKB)
+    lo, hi = [], []
     for i in range((L + FQT - 1) // FQT):
-        if not causal:
-            out.append(nkb - 1)
-            continue
-        ql = min(i * FQT + FQT - 1, L - 1)
-        kend = min((ql // tpf + 1) * tpf, L)
-        out.append(min((kend - 1) // FKB, nkb - 1))
-    return torch.tensor(out)
+        js = [j for j, (a, b) in enumerate(sw) if a <= i <= b]
+        assert js == list(range(js[0], js[-1] + 1)), "sweep ranges must give contiguous contributors"
+        lo.append(js[0])
+        hi.append(js[-1])
+    return torch.tensor(lo), torch.tensor(hi)
 
 
 FUSED_CASES = [
-    # (B, H, n_frames, tpf, causal)
-    (1, 2, 8, 64, True),  # 2 key blocks, 8 query tiles
-    (2, 3, 20, 64, True),  # 6 chains (< 8 XCD queues), 5 key blocks
-    (1, 2, 7, 65, True),  # ragged end, frames across tile seams (455 tokens)
-    (1, 1, 300, 1, True),  # token-causal: PARTIAL diagonal tiles, ragged last key block
-    (1, 2, 40, 64, False),  # unmasked (every block sweeps every tile)
-    (2, 8, 48, 64, True),  # 16 chains x 12 key blocks
+    # (B, H, n_frames, tpf, causal, window)
+    (1, 2, 8, 64, True, None),  # 2 key blocks, 8 query tiles
+    (2, 3, 20, 64, True, None),  # 6 chains (< 8 XCD queues), 5 key blocks
+    (1, 2, 7, 65, True, None),  # ragged end, frames across tile seams (455 tokens)
+    (1, 1, 300, 1, True, None),  # token-causal: PARTIAL diagonal tiles, ragged last key block
+    (1, 2, 40, 64, False, None),  # unmasked (every block sweeps every tile)
+    (2, 8, 48, 64, True, None),  # 16 chains x 12 key blocks
+    (1, 2, 48, 64, True, 16),  # dit_v4's local layers: a tile's first contributor is not block 0
+    (1, 2, 30, 65, True, 4),  # window of 4 frames across tile seams
+    (1, 2, 40, 64, False, 3),  # windowed, not causal (keys see queries on both sides)
+    (1, 1, 600, 1, True, 100),  # token-causal window: PARTIAL tiles on both edges
 ]
 
 
@@ -86,10 +101,10 @@ FUSED_CASES = [
 @pytest.mark.parametrize("case", FUSED_CASES)
 def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
     k = K()
-    B, H, nf, tpf, causal = case
+    B, H, nf, tpf, causal, window = case
     D, L = 64, nf * tpf
     q, kk, v, do = _inputs(B, H, L, D, 100)
-    mask = k.FrameMask(tpf, None, causal)
+    mask = k.FrameMask(tpf, window, causal)
     o, lse = k.attn_fwd(q, kk, v, H, D, mask)
     delta = _delta(o, do, H, D)
     got = [torch.full_like(q, float("nan")) for _ in range(3)]
@@ -101,7 +116,7 @@ def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
     k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, *split)
     # fp32 oracle
     qr, kr, vr = (t.cpu().float().view(B, L, H, D).transpose(1, 2).requires_grad_() for t in (q, kk, v))
-    m = R.frame_mask(L, L, tpf, None, None, causal=causal)
+    m = R.frame_mask(L, L, tpf, window, None, causal=causal)
     oref = R.attention(qr, kr, vr, m)
     oref.backward(do.cpu().float().view(B, L, H, D).transpose(1, 2))
     for name, g, s, ref in zip(("dq", "dk", "dv"), got, split, (qr.grad, kr.grad, vr.grad)):
@@ -110,16 +125,17 @@ def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
         assert rel(g, s) < 5e-3, name
 
 
-@pytest.mark.parametrize("case", [(2, 8, 48, 64, True), (1, 2, 40, 64, False), (1, 1, 300, 1, True)])
+@pytest.mark.parametrize("case", [(2, 8, 48, 64, True, None), (1, 2, 40, 64, False, None), (1, 1, 300, 1, True, None),
+                                  (1, 2, 48, 64, True, 16)])
 def test_attention_bwd_fused_deterministic(case):
     """Every query tile receives its key blocks' dQ parts in key-block order, so two runs -- and the
     write-through and the XCD-local hand-offs, which differ only in where the sums live, and the
     chain-group dequeue orders (variant bits 2-5) -- give the same bits."""
     k = K()
-    B, H, nf, tpf, causal = case
+    B, H, nf, tpf, causal, window = case
     D, L = 64, nf * tpf
     q, kk, v, do = _inputs(B, H, L, D, 200)
-    mask = k.FrameMask(tpf, None, causal)
+    mask = k.FrameMask(tpf, window, causal)
     o, lse = k.attn_fwd(q, kk, v, H, D, mask)
     delta = _delta(o, do, H, D)
     runs = []
@@ -135,20 +151,23 @@ def test_attention_bwd_fused_deterministic(case):
 
 
 @pytest.mark.parametrize("variant", [2, 3, 7])
-@pytest.mark.parametrize("shape", [(1, 24, 1536, 64, True), (2, 3, 20, 64, True), (1, 1, 300, 1, True),
-                                   (1, 2, 40, 64, False), (1, 8, 96, 65, True)])
+@pytest.mark.parametrize("shape", [(1, 24, 1536, 64, True, None), (2, 3, 20, 64, True, None), (1, 1, 300, 1, True, None),
+                                   (1, 2, 40, 64, False, None), (1, 8, 96, 65, True, None),
+                                   (1, 24, 1536, 64, True, 16), (1, 2, 30, 65, True, 4), (1, 2, 40, 64, False, 3),
+                                   (1, 1, 600, 1, True, 100)])
 def test_attention_bwd_fused_handoff_counts(shape, variant):
     """Counting form of the hand-off (variant bit 1): every key block adds 1.0 instead of its dQ
     part and the last one keeps the fp32 sum, so each of the 4,096 words of every query tile's sum
-    must equal the number of key blocks that see the tile -- a stale read or a lost add anywhere
-    shows as a smaller count.  Checked at the full dit_v4 shape (24 heads x 98,304 tokens, 1,536
-    tiles x 384 key blocks per head, every XCD queue busy), for both hand-off forms; the flags end
-    at the same counts."""
+    must equal the number of key blocks that sweep the tile -- a stale read or a lost add anywhere
+    shows as a smaller count, a hand-off that started from zeros too late or too early as another.
+    Checked at the full dit_v4 shapes (24 heads x 98,304 tokens, 1,536 tiles x 384 key blocks per
+    head, global and window 16), for both hand-off forms and the one-chain-at-a-time dequeue; the
+    flags end at one past each tile's last contributor."""
     k = K()
-    B, H, nf, tpf, causal = shape
+    B, H, nf, tpf, causal, window = shape
     D, L = 64, nf * tpf
     q, kk, v, do = _inputs(B, H, L, D, 300)
-    mask = k.FrameMask(tpf, None, causal)
+    mask = k.FrameMask(tpf, window, causal)
     lse = torch.zeros(B, H, L, device=DEV)
     delta = torch.zeros(B, H, L, device=DEV)
     dq, dk, dv = (torch.empty_like(q) for _ in range(3))
@@ -158,10 +177,12 @@ def test_attention_bwd_fused_handoff_counts(shape, variant):
     nchain, nt = B * H, (L + FQT - 1) // FQT
     fkb = _hdr(ws)[9].item()
     assert fkb in (128, 256)
-    want = (_jhi(L, tpf, causal, fkb) + 1).to(DEV)
+    jlo, jhi = _jrange(L, tpf, causal, window, fkb)
+    want_flag = (jhi + 1).to(DEV)
+    want_sum = (jhi - jlo + 1).to(DEV)  # every contributor adds 1.0, the first onto zeros
     flags = ws[256:256 + nchain * nt * 64].view(torch.int32).view(nchain, nt, 16)[:, :, 0]
-    assert torch.equal(flags, want[None, :].to(torch.int32).expand(nchain, nt))
+    assert torch.equal(flags, want_flag[None, :].to(torch.int32).expand(nchain, nt))
     acc = ws[256 + nchain * nt * 64:256 + nchain * nt * (64 + FQT * 64 * 4)].view(torch.float32)
     acc = acc.view(nchain, nt, FQT * 64)
-    bad = (acc != want[None, :, None].float()).sum().item()
+    bad = (acc != want_sum[None, :, None].float()).sum().item()
     assert bad == 0, f"{bad} accumulator words off"
