@@ -78,7 +78,13 @@ constexpr int SMEM_BYTES = MISC_OFF + 16;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
 constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
-constexpr int NACC = 4;                        // 16-B words per lane of a wave's 32 x 32 part of a tile's sum
+// dQ^T products: 0 = 32x32x16 MFMAs on waves 0-3 (one 32 d x 32 q tile each); 1 = 16x16x32 MFMAs
+// on all 8 waves (one 16 d x 32 q quarter each: 50 % more LDS bytes, no idle waves)
+#ifndef OWLK_FUSED_DQ16
+#define OWLK_FUSED_DQ16 0
+#endif
+constexpr bool DQ16 = OWLK_FUSED_DQ16;
+constexpr int NACC = DQ16 ? 2 : 4;  // 16-B words per lane of a wave's part of a tile's sum
 
 struct FusedP {
   const bf16 *q, *k, *v, *dout;
@@ -194,6 +200,10 @@ template <int N, typename A, typename B, typename C, typename D>
 DEV void lgkm4(A& a, B& b, C& c, D& d) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
 }
+template <int N, typename T>
+DEV void lgkm6(T& a, T& b, T& c, T& d, T& e, T& f) {
+  asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f) : "n"(N) : "memory");
+}
 template <typename F, int... I>
 DEV void static_for_(F&& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
@@ -274,8 +284,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const int L = p.L;
   char* kimg = smem + KIMG_OFF;
   // dQ^T of a tile: waves 0-3, one 32 x 32 tile each (d tile dt32, query tile qt32)
-  const bool dq_wave = w < 4;
+  const bool dq_wave = DQ16 || w < 4;
   const int dt32 = w & 1, qt32 = (w >> 1) & 1;
+  // DQ16: this wave's quarter of dQ^T: d tile dt (16), query tiles qt0, qt0 + 1 (16 each)
+  const int dt = w & 3, qt0 = 2 * (w >> 2);
+  const unsigned offk = tr16_lane_off(dt, lane), offs0 = tr16_lane_off(qt0, lane), offs1 = tr16_lane_off(qt0 + 1, lane);
   const unsigned acc_lane = (unsigned)(w * NACC * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
   int ok32a, ok32b, os32a, os32b;
   tr32_lane_off(dt32, lane, ok32a, ok32b);
@@ -420,8 +433,33 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     // 32 qt32 + (lane & 31); register 4 rr + e: d 32 dt32 + 8 rr + 4 h + e), else the fp32 sum
     // (sc1 write-through; plain in the local variant)
     f32x16 qacc;
+    f32x4 qa[2];  // DQ16
     auto store_dq = [&](int i) {
       const bool last = j >= tile_jhi(p, i);
+      if constexpr (DQ16) {
+        if (last && !counting) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int qrow = i * FQT + 16 * (qt0 + e) + c;
+            if (qrow < L) {
+              bf16x4 o4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o4[r] = (bf16)(qa[e][r] * -p.scale);  // dS accumulated negated
+              *(bf16x4*)(p.dq + b * p.sdqb + (long)qrow * p.lddq + head * 64 + 16 * dt + 4 * g) = o4;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int off = (int)(i * ACC_TILE_BYTES + acc_lane + e * 1024);
+            if constexpr (local)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, qa[e]), ars, off, 0, 0);
+            else
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, qa[e]), ars, off, 0, 16);
+          }
+        }
+        return;
+      }
       if (last && !counting) {
         const int qrow = i * FQT + 32 * qt32 + (lane & 31);
         if (qrow < L) {
@@ -461,6 +499,38 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       if constexpr (counting) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) qacc[e] += 1.f;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qa[e][r] += 1.f;
+        return;
+      }
+      if constexpr (DQ16) {
+        // dQ^T[16 d x 16 q] (two query tiles) += K^T[16 d x 32 keys] dS^T[32 keys x 16 q]: frag_tr16 at
+        // row0 = 32 kk (immediate kk * 4 KiB, + 2 KiB for the second 4-row group), pipelined as below
+        constexpr int NK = FKB / 32, PF = OWLK_FUSED_DQ_PF;
+        const unsigned sb0 = lds_addr(smem + DS_OFF + (i & 1) * DS_BYTES);
+        const unsigned ka = lds_addr(kimg) + offk, s0 = sb0 + offs0, s1 = sb0 + offs1;
+        s16x4 r[PF + 1][6];
+        auto rd = [&](auto kc) {
+          constexpr int k2 = decltype(kc)::value, sl = k2 % (PF + 1);
+          r[sl][0] = tr_rd<4096 * k2>(ka);
+          r[sl][1] = tr_rd<4096 * k2 + 2048>(ka);
+          r[sl][2] = tr_rd<4096 * k2>(s0);
+          r[sl][3] = tr_rd<4096 * k2 + 2048>(s0);
+          r[sl][4] = tr_rd<4096 * k2>(s1);
+          r[sl][5] = tr_rd<4096 * k2 + 2048>(s1);
+        };
+        static_for<PF>(rd);
+        static_for<NK>([&](auto kc) {
+          constexpr int k2 = decltype(kc)::value, sl = k2 % (PF + 1);
+          if constexpr (k2 + PF < NK) rd(std::integral_constant<int, k2 + PF>{});
+          constexpr int younger = 6 * (PF < NK - 1 - k2 ? PF : NK - 1 - k2);
+          lgkm6<younger>(r[sl][0], r[sl][1], r[sl][2], r[sl][3], r[sl][4], r[sl][5]);
+          const bf16x8 ak = join_tr(r[sl][0], r[sl][1]);
+          qa[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, join_tr(r[sl][2], r[sl][3]), qa[0], 0, 0, 0);
+          qa[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, join_tr(r[sl][4], r[sl][5]), qa[1], 0, 0, 0);
+        });
         return;
       }
       constexpr int NK = FKB / 16, PF = OWLK_FUSED_DQ_PF;
@@ -510,10 +580,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
         for (int e = 0; e < NACC; ++e) a[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
       }
+      if constexpr (DQ16) {
+        qa[0] = a[0];
+        qa[1] = a[1];
+      } else {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
+        for (int rr = 0; rr < NACC; ++rr)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) qacc[4 * rr + r] = a[rr][r];
+          for (int r = 0; r < 4; ++r) qacc[4 * rr + r] = a[rr][r];
+      }
     };
 
     for (int t = t_hi; t >= t_lo; --t) {
