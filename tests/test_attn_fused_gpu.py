@@ -94,6 +94,7 @@ FUSED_CASES = [
     (1, 2, 30, 65, True, 4),  # window of 4 frames across tile seams
     (1, 2, 40, 64, False, 3),  # windowed, not causal (keys see queries on both sides)
     (1, 1, 600, 1, True, 100),  # token-causal window: PARTIAL tiles on both edges
+    (2, 3, 30, 65, True, 4),  # batch 2 x 3 heads, windowed (mmdit_v2's 65-token frames)
 ]
 
 
