@@ -306,8 +306,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const int dch = (lane & 7) ^ swz_dual(drow);
   const unsigned offq = (unsigned)((drow * p.ldq + dch * 8) * 2), offd = (unsigned)((drow * p.ldo + dch * 8) * 2);
 
-  unsigned long long prof[4] = {0ull, 0ull, 0ull, 0ull};
+  // OWLK_FUSED_PROF: per-step phases {dq, main, vmwait, barrier} and per-item {dequeue, prologue,
+  // epilogue} (s_memtime cycles)
+  unsigned long long prof[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
   for (;;) {
+    const unsigned long long ca = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local)
     if (threadIdx.x == 0) {
       int chain = -1, jj = 0;
@@ -335,11 +338,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     __syncthreads();
     const int chain = __builtin_amdgcn_readfirstlane(sh_item[0]);
     const int j = __builtin_amdgcn_readfirstlane(sh_item[1]);
+    const unsigned long long cb = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     if (chain < 0) {
       if (OWLK_FUSED_PROF && lane == 0) {
-        unsigned long long* pp = (unsigned long long*)((char*)p.hdr + 128) + (w < 4 ? 0 : 4);
+        unsigned long long* pp = (unsigned long long*)((char*)p.hdr + 128) + (w < 4 ? 0 : 8);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) __hip_atomic_fetch_add(pp + e, prof[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int e = 0; e < 7; ++e) __hip_atomic_fetch_add(pp + e, prof[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
@@ -558,6 +562,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     issue(t_hi);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const unsigned long long cc = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
 
     // ready: the predecessor's sum of the tile whose dQ is formed next was found published at
     // mid-step of the tile's own step and is in flight to this wave's landing zone (waited for at
@@ -787,6 +792,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     }
 
     // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
+    const unsigned long long cd = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     if (!(OWLK_FUSED_EXP & 2) && dq_wave) {
       dq_begin(t_lo);
       dq_mfma(t_lo);
@@ -814,6 +820,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         *(bf16x4*)(pk + 16 * ds) = a4;
         *(bf16x4*)(pv + 16 * ds) = b4;
       }
+    }
+    if (OWLK_FUSED_PROF) {
+      const unsigned long long ce = __builtin_amdgcn_s_memtime();
+      prof[4] += cb - ca;
+      prof[5] += cc - cb;
+      prof[6] += ce - cd;
     }
   }
 }

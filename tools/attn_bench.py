@@ -113,15 +113,14 @@ def main():
                                                                      D ** -0.5, var, ws), args.iters))
             hw = ws[:256].view(torch.int32).cpu()
             err = hw[8].item()
-            pw = ws[128:192].view(torch.int64).cpu().tolist()
+            pw = ws[128:256].view(torch.int64).cpu().tolist()
             if any(pw):  # OWLK_FUSED_PROF builds: cycles per phase, dQ waves | other waves
-                tot = sum(pw[:4]) or 1
-                tot2 = sum(pw[4:]) or 1
-                print("  fused phases (s_memtime cycles, share of the sweep): dQ waves: " +
-                      ", ".join(f"{n} {v / tot:.3f}" for n, v in zip(("dq", "main", "vmwait", "barrier"), pw[:4])) +
-                      " | other waves: " +
-                      ", ".join(f"{n} {v / tot2:.3f}" for n, v in zip(("dq", "main", "vmwait", "barrier"), pw[4:])) +
-                      f" | cycles per wave-step {tot / 1:.3e} total", flush=True)
+                names = ("dq", "main", "vmwait", "barrier", "dequeue", "prologue", "epilogue")
+                for nm, part in (("dQ waves", pw[:7]), ("other waves", pw[8:15])):
+                    tot = sum(part) or 1
+                    print(f"  fused phases, {nm} (s_memtime cycles, share of the workgroup time): " +
+                          ", ".join(f"{n} {v / tot:.3f}" for n, v in zip(names, part)) +
+                          f" | {tot:.3e} cycles", flush=True)
             if hw[11].item():  # OWLK_FUSED_STATS builds: the last call's (xcd-local) hand-offs
                 print(f"  fused hand-offs (last call): {hw[10].item()} of {hw[11].item()} found the flag down at "
                       f"mid-step ({hw[10].item() / hw[11].item():.3f})", flush=True)
