@@ -57,6 +57,15 @@
 #define OWLK_FUSED_PROF 0
 #endif
 // software-pipeline depth of the 32x32 dQ products (k-steps of reads in flight ahead of the MFMA)
+// values formed from an opaque lane id at each use instead of kept across the sweep (bits: 1 the
+// ring's DMA offsets, 2 the dS image addresses, 4 the operand read addresses, 8 the mask rows and
+// the epilogue's keys); 0 = all kept (hipcc spills some of them)
+#ifndef OWLK_FUSED_REMAT
+#define OWLK_FUSED_REMAT 0
+#endif
+#ifndef OWLK_FUSED_DEQ_PF  // 1: an item's successor is claimed during its epilogue
+#define OWLK_FUSED_DEQ_PF 1
+#endif
 #ifndef OWLK_FUSED_DQ_PF
 #define OWLK_FUSED_DQ_PF 2
 #endif
@@ -170,6 +179,13 @@ DEV void dma4_sc1(unsigned lds, const void* base, unsigned off) {
                : "memory", "m0");
 }
 #pragma clang diagnostic pop
+// a copy the compiler cannot see through: values formed from it are formed where they are used
+// (hoisted out of the sweep, the dS image's 16 per-lane piece addresses were kept live and spilled)
+template <int BIT = 0>
+DEV unsigned opaque(unsigned x) {
+  if (!BIT || (OWLK_FUSED_REMAT & BIT)) asm volatile("" : "+v"(x));
+  return x;
+}
 template <int N>
 DEV void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -296,6 +312,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   // per-lane LDS byte offsets in a ring slot (row0 a multiple of 16 in the immediate): frag_row16
   // of k-step 0 / 1, frag_tr16 of column group ds, the lse2 / delta rows of lane group g
   const unsigned ro0 = row16_lane_off(0, lane), ro1 = row16_lane_off(1, lane);
+  // dS^T image pieces (8 B): row r = 32 w + 16 t2 + c, 16-B chunk ch = 4 qb + 2 e + (g >> 1), at
+  // r * 128 + ((ch ^ swz_dual(r)) << 4) + 8 (g & 1) = dsl + 2048 t2 + ((64 qb + 32 e) ^ dsx), as
+  // swz_dual(r) = swz_dual(c) (it repeats every 16 rows) and 64 qb + 32 e has only bits 5-6
+  const unsigned dsl = (unsigned)((32 * w + c) * 128 + 8 * (g & 1));
+  const unsigned dsx = (unsigned)((((g >> 1) ^ swz_dual(c)) << 4));
   const unsigned tro0 = tr16_lane_off(0, lane), tro1 = tr16_lane_off(1, lane), tro2 = tr16_lane_off(2, lane),
                  tro3 = tr16_lane_off(3, lane);
   if (blockIdx.x == 0 && threadIdx.x == 0) p.hdr[9] = FKB;  // for readers of the workspace (tests)
@@ -304,34 +325,49 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   // wave-instruction, swizzled source chunk)
   const int drow = 8 * w + (lane >> 3);
   const int dch = (lane & 7) ^ swz_dual(drow);
-  const unsigned offq = (unsigned)((drow * p.ldq + dch * 8) * 2), offd = (unsigned)((drow * p.ldo + dch * 8) * 2);
+  // (formed from an opaque lane id at each use: kept live across the sweep they were spilled, and
+  // each reload's vmcnt(0) drained the dQ stores before the ring's DMA)
+  auto row_off = [&](int ld) {
+    const int ln = (int)opaque<1>((unsigned)lane), r = 8 * w + (ln >> 3);
+    return (unsigned)((r * ld + (((ln & 7) ^ swz_dual(r)) * 8)) * 2);
+  };
 
   // OWLK_FUSED_PROF: per-step phases {dq, main, vmwait, barrier} and per-item {dequeue, prologue,
   // epilogue} (s_memtime cycles)
   unsigned long long prof[8] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+  // the item of the n-th claim on queue x: the queue's chains in groups of p.group (j-major inside
+  // a group): fewer chains at a time give each chain more workgroups, so a key block's successor
+  // follows closer behind and the chain's sums and Q / dO tiles are re-read fewer times (each
+  // generation of concurrent blocks re-sweeps the chain)
+  auto item_of = [&](int x, int n, int& chain, int& jj) {
+    const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
+    if (n >= cx * p.nkb) return false;
+    const int gfull = p.group * p.nkb, gi = n / gfull, m = n - gi * gfull;
+    const int gsz = cx - gi * p.group < p.group ? cx - gi * p.group : p.group;
+    chain = x + 8 * (gi * p.group + m % gsz);
+    jj = m / gsz;
+    return true;
+  };
+  // a claim on the queues of XCDs xcc + d0, xcc + d0 + 1, ... (only this XCD's when local)
+  auto claim = [&](int d0, int& chain, int& jj) {
+    chain = -1;
+    jj = 0;
+    for (int d = d0; d < (local ? 1 : 8) && chain < 0; ++d) {
+      const int x = (int)((xcc + d) & 7);
+      const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
+      if (cx == 0) continue;
+      if (__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cx * p.nkb) continue;
+      item_of(x, __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), chain, jj);
+    }
+  };
+  if (OWLK_FUSED_DEQ_PF && threadIdx.x == 0) claim(0, sh_item[0], sh_item[1]);
   for (;;) {
     const unsigned long long ca = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
-    // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local)
-    if (threadIdx.x == 0) {
-      int chain = -1, jj = 0;
-      for (int d = 0; d < (local ? 1 : 8) && chain < 0; ++d) {
-        const int x = (int)((xcc + d) & 7);
-        const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
-        if (cx == 0) continue;
-        const int total = cx * p.nkb;
-        if (__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total) continue;
-        const int n = __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n < total) {
-          // the queue's chains in groups of p.group (j-major inside a group): fewer chains at a
-          // time give each chain more workgroups, so a key block's successor follows closer behind
-          // and the chain's sums and Q / dO tiles are re-read fewer times (each generation of
-          // concurrent blocks re-sweeps the chain)
-          const int gfull = p.group * p.nkb, gi = n / gfull, m = n - gi * gfull;
-          const int gsz = cx - gi * p.group < p.group ? cx - gi * p.group : p.group;
-          chain = x + 8 * (gi * p.group + m % gsz);
-          jj = m / gsz;
-        }
-      }
+    // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local);
+    // OWLK_FUSED_DEQ_PF: claimed during the previous item's epilogue
+    if (!OWLK_FUSED_DEQ_PF && threadIdx.x == 0) {
+      int chain, jj;
+      claim(0, chain, jj);
       sh_item[0] = chain;
       sh_item[1] = jj;
     }
@@ -377,8 +413,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       char* buf = smem + (t & 1) * RING_SLOT;
       const int q0 = t * FQT;
       if (q0 + FQT <= L) {
-        dma16(lds_addr(buf + 8 * w * 128), Q + (long)q0 * p.ldq, offq);
-        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)q0 * p.ldo, offd);
+        dma16(lds_addr(buf + 8 * w * 128), Q + (long)q0 * p.ldq, row_off(p.ldq));
+        dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)q0 * p.ldo, row_off(p.ldo));
       } else {
         int gr = q0 + drow;
         gr = gr < L ? gr : L - 1;
@@ -614,7 +650,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       // a tile's S / dP operands of query rows 32 qb .. + 31 (lse2, delta rows, Q and dO
       // fragments), by asm in the order they are consumed: 12 LDS reads
       const unsigned sbase = lds_addr(smem + (t & 1) * RING_SLOT);
-      const unsigned a_r0 = sbase + ro0, a_r1 = sbase + ro1, a_l = sbase + 16 * g;
+      const unsigned a_r0 = sbase + opaque<4>(ro0), a_r1 = sbase + opaque<4>(ro1), a_l = sbase + 16 * (opaque<4>((unsigned)lane) >> 4);
       f32x4 lr[2], dr[2];
       bf16x8 aq[2][2], ad[2][2];  // [k step][16-row query tile]
       auto issue_a = [&](auto qbc) {
@@ -649,14 +685,20 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const bool poll = j > tile_jlo(p, t) && dq_wave && !(OWLK_FUSED_EXP & 1);
       if (poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
 
-      char* dsw = smem + DS_OFF + (t & 1) * DS_BYTES;
-      unsigned long long bh[2] = {0ull, 0ull};
+      const unsigned dsw = lds_addr(smem + DS_OFF + (t & 1) * DS_BYTES) + dsl;
+      auto ds_put = [&](int t2, int qb, int e, bf16x4 v) {
+        *(AS3 bf16x4*)(uintptr_t)(dsw + 2048 * t2 + ((unsigned)(64 * qb + 32 * e) ^ opaque<2>(dsx))) = v;
+      };
+      unsigned bh[2] = {0u, 0u};  // bit 4 m + r: query row q0 + 16 m + 4 g + r of key t2
       if (masked) {  // query rows [frame(key) tpf, L) (causal) / [0, L) of the tile, per key
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2) {
-          const int fk = frame(p, my_k[t2]);
-          const long lo = (long)q_lo_frame(p, fk) * p.tpf, hi = q_hi_end(p, fk);
-          bh[t2] = my_k[t2] < L ? range_bits(lo - q0, hi - q0) >> (4 * g) : 0ull;
+          // the key from an opaque lane id: its row range is formed here, not kept across the sweep
+          const int k = kw0 + 16 * t2 + (int)(opaque<8>((unsigned)lane) & 15), fk = frame(p, k);
+          const int lo = q_lo_frame(p, fk) * p.tpf - q0, hi = (int)q_hi_end(p, fk) - q0;
+          const unsigned long long b64 = k < L ? range_bits(lo, hi) >> (4 * g) : 0ull;
+          bh[t2] = (unsigned)(b64 & 0xF) | (unsigned)((b64 >> 12) & 0xF0) | (unsigned)((b64 >> 24) & 0xF00) |
+                   (unsigned)((b64 >> 36) & 0xF000);
         }
       }
       bool loads_out = false;
@@ -665,14 +707,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         if (kind == TILE_EMPTY) {
           // no allowed pair for this wave's keys: its rows of the dS image are zero
 #pragma unroll
-          for (int t2 = 0; t2 < 2; ++t2) {
-            const int r = 32 * w + 16 * t2 + c;
+          for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const int ch = 4 * qb + 2 * hh + (g >> 1);
-              *(bf16x4*)(dsw + r * 128 + ((ch ^ swz_dual(r)) << 4) + 8 * (g & 1)) = bf16x4{};
-            }
-          }
+            for (int e = 0; e < 2; ++e) ds_put(t2, qb, e, bf16x4{});
         } else {
           // S / dP (12 reads in flight, oldest first: lse2 / delta rows, then k step 0, 1).  Issued
           // here, not earlier: holding them across the step's control flow overflows the 256-VGPR
@@ -707,10 +744,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
             tq[ds][2] = tr_rd<128 * 32 * qb>(a);
             tq[ds][3] = tr_rd<128 * 32 * qb + 2048>(a);
           };
-          rd_t(std::integral_constant<int, 0>{}, sbase + tro0);
-          rd_t(std::integral_constant<int, 1>{}, sbase + tro1);
-          rd_t(std::integral_constant<int, 2>{}, sbase + tro2);
-          rd_t(std::integral_constant<int, 3>{}, sbase + tro3);
+          rd_t(std::integral_constant<int, 0>{}, sbase + opaque<4>(tro0));
+          rd_t(std::integral_constant<int, 1>{}, sbase + opaque<4>(tro1));
+          rd_t(std::integral_constant<int, 2>{}, sbase + opaque<4>(tro2));
+          rd_t(std::integral_constant<int, 3>{}, sbase + opaque<4>(tro3));
 #pragma unroll
           for (int qs = 0; qs < 2; ++qs)
 #pragma unroll
@@ -720,8 +757,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           if (masked) {
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2) {
-              apply_bits4<32 * qb>(st[0][t2], bh[t2], 0.f);
-              apply_bits4<32 * qb + 16>(st[1][t2], bh[t2], 0.f);
+              apply_bits4<8 * qb>(st[0][t2], bh[t2], 0.f);
+              apply_bits4<8 * qb + 4>(st[1][t2], bh[t2], 0.f);
             }
           }
           bf16x8 pf[2], sf[2];
@@ -738,13 +775,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           // 32 qb + 4 g .. + 3 (elements 0..3) and 32 qb + 16 + 4 g .. + 3 (elements 4..7) of key c
 #pragma unroll
           for (int t2 = 0; t2 < 2; ++t2) {
-            const int r = 32 * w + 16 * t2 + c;
-            const bf16x4 lo4 = __builtin_shufflevector(sf[t2], sf[t2], 0, 1, 2, 3);
-            const bf16x4 hi4 = __builtin_shufflevector(sf[t2], sf[t2], 4, 5, 6, 7);
-            const int ch0 = 4 * qb + (g >> 1), ch1 = ch0 + 2;
             if (!(OWLK_FUSED_EXP & 4)) {
-              *(bf16x4*)(dsw + r * 128 + ((ch0 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = lo4;
-              *(bf16x4*)(dsw + r * 128 + ((ch1 ^ swz_dual(r)) << 4) + 8 * (g & 1)) = hi4;
+              ds_put(t2, qb, 0, __builtin_shufflevector(sf[t2], sf[t2], 0, 1, 2, 3));
+              ds_put(t2, qb, 1, __builtin_shufflevector(sf[t2], sf[t2], 4, 5, 6, 7));
             }
           }
           // dV / dK (the dS stores above are younger than every read waited for: the counts
@@ -763,7 +796,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         if constexpr (qb == 0) {
           if (poll) {  // the flag polled at the top has had half a tile to arrive
             vm_wait<0>();  // the dQ stores, the ring's DMA and the flag poll, in issue order
-            ready = __builtin_amdgcn_readfirstlane(*(const int*)(flagl + lane * 4)) >= j;
+            ready = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= j;  // 64 copies of one word
             if (ready) {
               load_acc(t);
               loads_out = true;
@@ -793,22 +826,35 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 
     // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
     const unsigned long long cd = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
-    if (!(OWLK_FUSED_EXP & 2) && dq_wave) {
-      dq_begin(t_lo);
+    const bool dq_epi = !(OWLK_FUSED_EXP & 2) && dq_wave;
+    if (dq_epi) dq_begin(t_lo);
+    // the next item's claim on this XCD's queue: its return is waited for with the dQ stores
+    int npf = 0;
+    if (OWLK_FUSED_DEQ_PF && threadIdx.x == 0)
+      npf = __hip_atomic_fetch_add(p.hdr + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dq_epi) {
       dq_mfma(t_lo);
       store_dq(t_lo);
     }
     vm_wait<0>();
     __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
       __hip_atomic_store(flg + t_lo * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (OWLK_FUSED_DEQ_PF) {
+        int nc = -1, nj = 0;
+        if (!item_of((int)xcc, npf, nc, nj)) claim(1, nc, nj);
+        sh_item[0] = nc;  // read after the next item's first barrier
+        sh_item[1] = nj;
+      }
+    }
 
     // dK[key][d], dV[key][d]: this lane holds d = 16 ds + 4 g + r of its two keys
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
-      if (my_k[t2] >= L) continue;
-      bf16* pk = p.dk + b * p.sdkb + (long)my_k[t2] * p.lddk + head * 64 + 4 * g;
-      bf16* pv = p.dv + b * p.sdvb + (long)my_k[t2] * p.lddv + head * 64 + 4 * g;
+      const int k = kw0 + 16 * t2 + (int)(opaque<8>((unsigned)lane) & 15);
+      if (k >= L) continue;
+      bf16* pk = p.dk + b * p.sdkb + (long)k * p.lddk + head * 64 + 4 * g;
+      bf16* pv = p.dv + b * p.sdvb + (long)k * p.lddv + head * 64 + 4 * g;
 #pragma unroll
       for (int ds = 0; ds < 4; ++ds) {
         bf16x4 a4, b4;
