@@ -63,6 +63,9 @@
 #ifndef OWLK_FUSED_REMAT
 #define OWLK_FUSED_REMAT 0
 #endif
+#ifndef OWLK_FUSED_KV_STAGE  // 1: dK / dV stored as whole rows through LDS
+#define OWLK_FUSED_KV_STAGE 1
+#endif
 #ifndef OWLK_FUSED_DEQ_PF  // 1: an item's successor is claimed during its epilogue
 #define OWLK_FUSED_DEQ_PF 1
 #endif
@@ -596,7 +599,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     };
 
     issue(t_hi);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    vm_wait<0>();
     __syncthreads();
     const unsigned long long cc = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
 
@@ -848,6 +851,40 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       }
     }
 
+#if OWLK_FUSED_KV_STAGE
+    // dK, dV through this wave's 8 KiB of the (now free) dS images, stored as whole 128-B rows with
+    // 16-B stores (lane-held 8-B pieces were 16 stores per lane, whose tail the next item's
+    // prologue waits for: vmcnt counts stores).  Row r = key kw0 + r, 16-B chunk x at x ^ (r & 7)
+    {
+      char* stg = smem + DS_OFF + w * 8192;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int r = 16 * t2 + c;
+#pragma unroll
+        for (int ds = 0; ds < 4; ++ds) {  // this lane: d = 16 ds + 4 g + e of key r
+          bf16x4 a4, b4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a4[e] = (bf16)(dk[ds][t2][e] * -p.scale);  // dS was accumulated negated
+            b4[e] = (bf16)dv[ds][t2][e];
+          }
+          const int off = r * 128 + (((2 * ds + (g >> 1)) ^ (r & 7)) << 4) + 8 * (g & 1);
+          *(bf16x4*)(stg + off) = a4;
+          *(bf16x4*)(stg + 4096 + off) = b4;
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int r = 8 * it + (lane >> 3), x = lane & 7, k = kw0 + r;
+        const int off = r * 128 + ((x ^ (r & 7)) << 4);
+        const bf16x8 vk = *(const bf16x8*)(stg + off), vv = *(const bf16x8*)(stg + 4096 + off);
+        if (k < L) {
+          *(bf16x8*)(p.dk + b * p.sdkb + (long)k * p.lddk + head * 64 + 8 * x) = vk;
+          *(bf16x8*)(p.dv + b * p.sdvb + (long)k * p.lddv + head * 64 + 8 * x) = vv;
+        }
+      }
+    }
+#else
     // dK[key][d], dV[key][d]: this lane holds d = 16 ds + 4 g + r of its two keys
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
@@ -867,6 +904,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         *(bf16x4*)(pv + 16 * ds) = b4;
       }
     }
+#endif
     if (OWLK_FUSED_PROF) {
       const unsigned long long ce = __builtin_amdgcn_s_memtime();
       prof[4] += cb - ca;

@@ -497,6 +497,9 @@ struct F16Cfg {
 };
 // KTT keys per swept tile: 64, or 128 (D 64 long sweeps: a two-slot ring of 32 KiB tiles, the
 // per-tile fixed costs paid once per 144 MFMAs)
+#ifndef OWLK_FWD_STAGE  // 1: D = 64 output rows stored whole through LDS
+#define OWLK_FWD_STAGE 1
+#endif
 template <int D, bool RS, int KTT = KT, int NQ = F16Cfg<D>::NQ>
 __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
   using C = Cfg<D>;
@@ -729,6 +732,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
     OWLK_BARRIER();
   }
 
+  // D = 64: O goes through this wave's 8 KiB of the (drained) ring and is stored as whole 128-B rows
+  // with 16-B stores, 8 per lane instead of 16 lane-held 8-B pieces (the store tail ends the
+  // workgroup).  Row r = query r0 + r, 16-B chunk x at x ^ (r & 7)
+  constexpr bool STAGE = D == 64 && OWLK_FWD_STAGE && NQ * 16 * 128 * 4 <= NBUF * TILEB;
+  char* stg = smem + w * (NQ * 16 * 128);
 #pragma unroll
   for (int t4 = 0; t4 < NQ; ++t4) {
     float ltot;
@@ -738,8 +746,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
       ltot = lrow[t4] + __shfl_xor(lrow[t4], 16, 64);
       ltot += __shfl_xor(ltot, 32, 64);
     }
-    if (my_q[t4] < p.Lq) {
-      const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+    const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+    if constexpr (STAGE) {
+      const int r = 16 * t4 + c;
+#pragma unroll
+      for (int ds = 0; ds < F::NDS; ++ds) {
+        bf16x4 v4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[ds][t4][e] * inv);
+        *(bf16x4*)(stg + r * 128 + (((2 * ds + (g >> 1)) ^ (r & 7)) << 4) + 8 * (g & 1)) = v4;
+      }
+      if (my_q[t4] < p.Lq && g == 0)
+        p.lse[(b * p.H + head) * p.Lq + my_q[t4]] = ltot > 0.f ? __log2f(ltot) : -INFINITY;
+    } else if (my_q[t4] < p.Lq) {
       bf16* O = p.o + b * p.sob + my_q[t4] * p.ldo + head * D + 4 * g;
 #pragma unroll
       for (int ds = 0; ds < F::NDS; ++ds) {
@@ -749,6 +768,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
         *(bf16x4*)(O + 16 * ds) = v4;
       }
       if (g == 0) p.lse[(b * p.H + head) * p.Lq + my_q[t4]] = ltot > 0.f ? __log2f(ltot) : -INFINITY;
+    }
+  }
+  if constexpr (STAGE) {
+#pragma unroll
+    for (int it = 0; it < NQ * 2; ++it) {
+      const int r = 8 * it + (lane >> 3), x = lane & 7;
+      const long q = r0 + r;
+      const bf16x8 v = *(const bf16x8*)(stg + r * 128 + ((x ^ (r & 7)) << 4));
+      if (q < p.Lq) *(bf16x8*)(p.o + b * p.sob + q * p.ldo + head * D + 8 * x) = v;
     }
   }
 }
