@@ -32,6 +32,9 @@
 //
 // Forward progress: items are dequeued in increasing key-block order per chain from per-XCD atomic
 // queues; an item waits only on its chain predecessor, which a running workgroup dequeued earlier.
+// A workgroup claims its next item during its current item's epilogue: the held claim is later in
+// its queue than the holder's running item, so the running item earliest in its queue always has a
+// predecessor that is done or running.
 // Spins are bounded by the real-time clock (error word in the workspace header).
 #include <utility>
 
