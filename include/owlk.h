@@ -183,7 +183,9 @@ int owlk_attn_bwd_dq(const void* q, long ldq, long sqb, const void* k, long ldk,
                      float scale, long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
                      const int* run_start, const int* doc, long fstride, void* stream);
 
-/* Single-pass backward (head_dim 64, document-free frame masks, windowed or not, Lq == Lkv == L): the same
+/* Single-pass backward (head_dim 64, Lq == Lkv == L; frame masks windowed or not, and causal masks of packed
+ * documents given as kv_lo / q_hi alone, every document one run of frames -- run_start / doc must be
+ * null, as owlk_attn_bwd's runs form): the same
  * outputs as owlk_attn_bwd from ONE kernel -- the compiled flex_attention backward of
  * attn.py:13-16,106-109 is likewise one pass.  Each 256-key block forms S and dP once and adds its
  * dQ part to a per-query-tile fp32 sum in the workspace in key-block order (ordered hand-off, no

@@ -89,7 +89,8 @@ constexpr int DS_BYTES = FKB * 128;
 constexpr int ACC_OFF = DS_OFF + 2 * DS_BYTES;  // per wave 2 KiB: its part of a tile's fp32 sum
 constexpr int FLAGL_OFF = ACC_OFF + 8 * 2048;    // per wave 256 B: a polled flag word (64 copies)
 constexpr int MISC_OFF = FLAGL_OFF + 8 * 256;
-constexpr int SMEM_BYTES = MISC_OFF + 16;
+constexpr int JLO_OFF = MISC_OFF + 16;          // packed documents: per ring slot, its tile's first contributor
+constexpr int SMEM_BYTES = JLO_OFF + 2 * 256;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
 constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
@@ -118,6 +119,12 @@ struct FusedP {
   char* acc;   // [nchain][ntiles][ACC_TILE_BYTES]
   int variant;
   int group;  // chains of a queue taken at a time (>= 1)
+  // packed documents (causal, every document one run of frames; attn_common.hpp runs_mode): key
+  // frame fk is seen by query frames fk .. q_hi[fk], query frame fq sees key frames kv_lo[fq] .. fq
+  const int *kv_lo, *q_hi;  // [B][fstride], window folded in
+  long fstride;
+  int* jlo;                  // [B][jlo_stride]: each query tile's first contributing key block
+  int jlo_stride;
 };
 
 DEV unsigned xcc_id() {
@@ -275,6 +282,22 @@ DEV int tile_jhi(const FusedP& p, int i) {
   return j < p.nkb - 1 ? j : p.nkb - 1;
 }
 
+// Packed documents: q_hi is non-decreasing (runs are contiguous, the window end is fq + W - 1), so
+// block j's sweep still ends at its last key's q_hi, and q_hi[fk] >= fq <=> fk >= kv_lo[fq] makes
+// min{j : sweep_hi(j) >= i} the block of key kv_lo[frame(i FQT)] tpf (fused_jlo_k, read per tile
+// from the ring slot: no global load inside the sweep)
+DEV long q_hi_end_runs(const FusedP& p, const int* qh, int fk) {
+  const long e = (long)(qh[fk] + 1) * p.tpf;
+  return e < p.L ? e : p.L;
+}
+__global__ void fused_jlo_k(FusedP p, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+  if (b >= B || i >= p.jlo_stride) return;
+  int v = 0;
+  if (i < p.ntiles) v = (int)((long)p.kv_lo[b * p.fstride + frame(p, i * FQT)] * p.tpf / FKB);
+  p.jlo[(long)b * p.jlo_stride + i] = v;
+}
+
 // bounded poll of a flag word (every lane loads the same word: one request), sc1 loads
 DEV bool wait_flag(const int* f, int want, int* err) {
   if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= want)
@@ -294,7 +317,7 @@ DEV bool wait_flag(const int* f, int want, int* err) {
   }
 }
 
-template <bool LOCAL, bool COUNTING>
+template <bool LOCAL, bool COUNTING, bool RUNS = false>
 __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   // ONE __shared__ object (see attn_bwd.hip: a second one makes hipcc drain the DMA ring)
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
@@ -402,8 +425,20 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
         p.acc + (long)chain * p.ntiles * ACC_TILE_BYTES, (short)0, p.ntiles * ACC_TILE_BYTES, 0x00020000);
     const int k0 = j * FKB, kw0 = k0 + 32 * w;
-    const int t_hi = sweep_hi(p, j);
+    const int* qh = RUNS ? p.q_hi + b * p.fstride : nullptr;  // this chain's sample
+    const int* jlo_row = RUNS ? p.jlo + (long)b * p.jlo_stride : nullptr;
+    int t_hi = sweep_hi(p, j);
+    if (RUNS) {
+      const int k1 = k0 + FKB - 1 < L ? k0 + FKB - 1 : L - 1;
+      t_hi = (int)((q_hi_end_runs(p, qh, frame(p, k1)) - 1) / FQT);
+    }
     const int t_lo = sweep_lo(p, j);
+    // the tile's first contributor: packed documents read it from the tile's ring slot (landed with
+    // the tile; a slot is re-filled only after its tile's last use)
+    auto jlo_at = [&](int i) {
+      if constexpr (RUNS) return __builtin_amdgcn_readfirstlane(*(const int*)(smem + JLO_OFF + (i & 1) * 256));
+      else return tile_jlo(p, i);
+    };
 
     // ---- K image of the item (unscaled K: the dQ^T A operand), 4 wave-instructions per wave
 #pragma unroll
@@ -431,6 +466,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         const int src = q0 + lane < L ? lane : L - 1 - q0;
         dma4(lds_addr(buf + 2 * TILE_BYTES + w * FQT * 4), (w ? DLT : LSE) + q0, (unsigned)(src * 4));
       }
+      if (RUNS && w == 2) dma4(lds_addr(smem + JLO_OFF + (t & 1) * 256), jlo_row + t, (unsigned)(lane * 4));
     };
 
     // this lane's two keys (column c of the wave's two 16-key tiles): k' = bf16(-c k), v' = -v
@@ -461,9 +497,19 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     // none of them sees, else PARTIAL
     const bool wave_live = kw0 < L;
     const int wfk0 = frame(p, kw0), wfk1 = frame(p, kw0 + 31 < L ? kw0 + 31 : L - 1);
-    const long seen_lo = (long)q_lo_frame(p, wfk0) * p.tpf, seen_hi = q_hi_end(p, wfk1);  // any key
+    const long seen_lo = (long)q_lo_frame(p, wfk0) * p.tpf,
+               seen_hi = RUNS ? q_hi_end_runs(p, qh, wfk1) : q_hi_end(p, wfk1);  // any key
     int full_lo = (int)(((long)q_lo_frame(p, wfk1) * p.tpf + FQT - 1) / FQT);
-    int full_hi = (int)(q_hi_end(p, wfk0) / FQT);  // exclusive: whole tiles only
+    int full_hi = (int)((RUNS ? q_hi_end_runs(p, qh, wfk0) : q_hi_end(p, wfk0)) / FQT);  // exclusive: whole tiles only
+    // packed documents: this lane's keys' row ends, for the PARTIAL tiles' masks
+    int khi[2] = {0, 0};
+    if (RUNS) {
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int k = kw0 + 16 * t2 + c;
+        khi[t2] = k < L ? (int)q_hi_end_runs(p, qh, frame(p, k)) : 0;
+      }
+    }
     if (full_hi > L / FQT) full_hi = L / FQT;
     if (!wave_live || kw0 + 32 > L) full_lo = full_hi = 0;
     full_lo = __builtin_amdgcn_readfirstlane(full_lo);
@@ -614,7 +660,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       f32x4 a[NACC];
 #pragma unroll
       for (int e = 0; e < NACC; ++e) a[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (j > tile_jlo(p, i) && !(OWLK_FUSED_EXP & 1)) {
+      if (j > jlo_at(i) && !(OWLK_FUSED_EXP & 1)) {
         if (OWLK_FUSED_STATS && lane == 0) {
           __hip_atomic_fetch_add(p.hdr + 11, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -688,7 +734,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const unsigned long long c1 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dma = t - 1 >= t_lo;
       if (dma) issue(t - 1);
-      const bool poll = j > tile_jlo(p, t) && dq_wave && !(OWLK_FUSED_EXP & 1);
+      const bool poll = j > jlo_at(t) && dq_wave && !(OWLK_FUSED_EXP & 1);
       if (poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
 
       const unsigned dsw = lds_addr(smem + DS_OFF + (t & 1) * DS_BYTES) + dsl;
@@ -701,7 +747,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         for (int t2 = 0; t2 < 2; ++t2) {
           // the key from an opaque lane id: its row range is formed here, not kept across the sweep
           const int k = kw0 + 16 * t2 + (int)(opaque<8>((unsigned)lane) & 15), fk = frame(p, k);
-          const int lo = q_lo_frame(p, fk) * p.tpf - q0, hi = (int)q_hi_end(p, fk) - q0;
+          const int lo = q_lo_frame(p, fk) * p.tpf - q0, hi = (RUNS ? khi[t2] : (int)q_hi_end(p, fk)) - q0;
           const unsigned long long b64 = k < L ? range_bits(lo, hi) >> (4 * g) : 0ull;
           bh[t2] = (unsigned)(b64 & 0xF) | (unsigned)((b64 >> 12) & 0xF0) | (unsigned)((b64 >> 24) & 0xF00) |
                    (unsigned)((b64 >> 36) & 0xF000);
@@ -949,7 +995,9 @@ static long fused_tiles(long L) { return (L + FQT - 1) / FQT; }
 extern "C" long owlk_attn_bwd_fused_ws_bytes(long B, int H, long L, int head_dim) {
   if (head_dim != 64 || B <= 0 || H <= 0 || L <= 0) return 0;
   const long nchain = B * H, nt = fused_tiles(L);
-  return HDR_BYTES + nchain * nt * (long)(FLAG_STRIDE * 4) + nchain * nt * (long)ACC_TILE_BYTES;
+  // header | flags | fp32 sums | packed documents' first contributor per (sample, tile), 64 words of
+  // slack per sample (the ring's 256-B DMA of a tile's word)
+  return HDR_BYTES + nchain * nt * (long)(FLAG_STRIDE * 4) + nchain * nt * (long)ACC_TILE_BYTES + B * (nt + 64) * 4L;
 }
 
 extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void* k, long ldk, long skb,
@@ -964,7 +1012,9 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   OWLK_REQUIRE(ldq < (1L << 31) && ldk < (1L << 31) && ldv < (1L << 31) && ldo < (1L << 31) && lddq < (1L << 31) &&
                    lddk < (1L << 31) && lddv < (1L << 31),
                "attn_bwd_fused: row strides too large");
-  OWLK_REQUIRE(!kv_lo && !q_hi && !run_start && !doc, "attn_bwd_fused: document-free masks only");
+  const bool runs = kv_lo || q_hi;
+  OWLK_REQUIRE(!run_start && !doc && (!runs || (kv_lo && q_hi && causal && fstride > 0)),
+               "attn_bwd_fused: document masks only as packed runs (kv_lo / q_hi, causal)");
   OWLK_REQUIRE(L < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_bwd_fused: sequence too long");
   OWLK_REQUIRE(fused_tiles(L) * (long)ACC_TILE_BYTES < (1L << 31), "attn_bwd_fused: sequence too long");
   OWLK_REQUIRE(B * H < (1L << 24), "attn_bwd_fused: too many heads");
@@ -997,6 +1047,11 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   p.acc = (char*)ws + HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4;
   p.variant = variant;
   p.group = (variant >> 2) & 15 ? (variant >> 2) & 15 : 1 << 20;  // variant bits 2-5; 0 = all of the queue's chains
+  p.kv_lo = kv_lo;
+  p.q_hi = q_hi;
+  p.fstride = fstride;
+  p.jlo_stride = p.ntiles + 64;
+  p.jlo = (int*)(p.acc + (long)p.nchain * p.ntiles * ACC_TILE_BYTES);
   hipStream_t s = (hipStream_t)stream;
   // counters, error word and flags are zero on entry (one memset node, 16-B multiple from the start)
   if (hipMemsetAsync(ws, 0, (size_t)(HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4), s) != hipSuccess)
@@ -1006,6 +1061,16 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   const dim3 grid((unsigned)fused_grid(dev));
   // the XCD-local hand-off only on an 8-XCC device (else: write-through)
   if ((variant & 1) && !all_xcds_present(dev)) variant &= ~1;
+  if (runs) {
+    OWLK_REQUIRE(!(variant & 2), "attn_bwd_fused: no counting mode with documents");
+    const dim3 gj((unsigned)((p.jlo_stride + 255) / 256), (unsigned)B);
+    hipLaunchKernelGGL(fused_jlo_k, gj, dim3(256), 0, s, p, (int)B);
+    if (variant & 1)
+      hipLaunchKernelGGL((attn_bwd_fused_k<true, false, true>), grid, dim3(512), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_bwd_fused_k<false, false, true>), grid, dim3(512), 0, s, p);
+    return owlk::check_launch("attn_bwd_fused");
+  }
   switch (variant & 3) {
     case 0: hipLaunchKernelGGL((attn_bwd_fused_k<false, false>), grid, dim3(512), 0, s, p); break;
     case 1: hipLaunchKernelGGL((attn_bwd_fused_k<true, false>), grid, dim3(512), 0, s, p); break;

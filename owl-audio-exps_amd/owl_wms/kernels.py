@@ -431,12 +431,17 @@ def _bwd_side_stream(device, D, mask):
 
 def fused_bwd_variant(D, mask):
     """owlk_attn_bwd_fused variant for this layer, or None for the two-kernel backward.  The single
-    pass serves head_dim 64 with a document-free mask, windowed or not (dit_v4's layers);
+    pass serves head_dim 64 with a document-free mask, windowed or not (dit_v4's layers), and causal
+    masks of packed documents (every document one run of frames: sequence packing; OWLK_BWD_FUSED_DOCS
+    = 0 sends those to the two kernels);
     OWLK_BWD_FUSED = 0 turns it off, 1 takes the write-through hand-off, 2 (default) keeps each
     chain's dQ sums in one XCD's L2 (the library runs it write-through on a device without 8 XCCs;
     include/owlk.h)."""
     env = os.environ.get("OWLK_BWD_FUSED", "2")
-    if env == "0" or D != 64 or mask.arrays is not None or mask.q_offset != 0:
+    if env == "0" or D != 64 or mask.q_offset != 0:
+        return None
+    if mask.arrays is not None and not (mask.arrays.get("runs") and mask.causal
+                                        and os.environ.get("OWLK_BWD_FUSED_DOCS", "1") != "0"):
         return None
     # windowed layers too, unless OWLK_BWD_FUSED_LOCAL = 0
     if mask.window is not None and os.environ.get("OWLK_BWD_FUSED_LOCAL", "1") == "0":
@@ -460,9 +465,8 @@ def attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, varia
          ptr(v), v.stride(1), v.stride(0), ptr(do), do.stride(1), do.stride(0), ptr(lse), ptr(delta),
          ptr(dq), dq.stride(1), dq.stride(0), ptr(dk), dk.stride(1), dk.stride(0),
          ptr(dv), dv.stride(1), dv.stride(0), B, H, L, D, float(scale),
-         mask.tpf, 0 if mask.window is None else int(mask.window), int(mask.causal), None, None, None, None, 0,
-         ptr(ws), ws.numel(), int(variant), stream(),
-         key=f"attn_bwd_fused[w{mask.window}]", flops=lambda: 8.0 * D * H * B * mask_pairs(mask, L, L))
+         *mask.args(), ptr(ws), ws.numel(), int(variant), stream(),
+         key=f"attn_bwd_fused[w{mask.window}{'d' if mask.arrays is not None else ''}]", flops=lambda: 8.0 * D * H * B * mask_pairs(mask, L, L))
     return ws
 
 

@@ -187,3 +187,65 @@ def test_attention_bwd_fused_handoff_counts(shape, variant):
     acc = acc.view(nchain, nt, FQT * 64)
     bad = (acc != want_sum[None, :, None].float()).sum().item()
     assert bad == 0, f"{bad} accumulator words off"
+
+
+def _runs_doc(B, nf, lens, seed):
+    """[B, nf] doc ids as contiguous runs (sequence packing): sample b's documents have the lengths
+    lens[b] (frames), the last one filling the rest"""
+    doc = torch.zeros(B, nf, dtype=torch.int64)
+    for b in range(B):
+        f, d = 0, 0
+        for n in lens[b]:
+            doc[b, f:f + n] = d
+            f, d = f + n, d + 1
+        doc[b, f:] = d
+    return doc
+
+
+DOC_CASES = [
+    # (B, H, n_frames, tpf, window, document lengths per sample)
+    (1, 2, 24, 64, None, [[5, 9, 3]]),  # four documents, runs across key-block and tile seams
+    (2, 3, 20, 64, None, [[7], [2, 2, 11]]),  # per-sample layouts (each chain its own runs)
+    (1, 2, 30, 65, 4, [[10, 13]]),  # window folded into kv_lo / q_hi, 65-token frames
+    (1, 1, 300, 1, None, [[37, 100, 1, 62]]),  # token-causal: documents of 1..100 tokens
+    (2, 8, 48, 64, 16, [[12, 12, 12], [30]]),  # dit_v4's local layers over packed documents
+]
+
+
+@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("case", DOC_CASES)
+def test_attention_bwd_fused_packed_documents(case, variant, monkeypatch):
+    """Causal masks of packed documents (kv_lo / q_hi, the runs form): the single pass against the
+    fp32 oracle with the document predicate (attn.py:24-62) and against the two-kernel backward,
+    and bitwise equal across hand-off forms."""
+    k = K()
+    B, H, nf, tpf, window, lens = case
+    D, L = 64, nf * tpf
+    q, kk, v, do = _inputs(B, H, L, D, 400)
+    doc = _runs_doc(B, nf, lens, 0)
+    arrays = k.frame_arrays(doc.to(DEV), nf, window)
+    assert arrays["runs"]
+    mask = k.FrameMask(tpf, window, True, arrays=arrays)
+    assert k.fused_bwd_variant(D, mask) is not None
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+    delta = _delta(o, do, H, D)
+    got = [torch.full_like(q, float("nan")) for _ in range(3)]
+    ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *got, D ** -0.5, variant)
+    torch.cuda.synchronize()
+    assert _hdr(ws)[8].item() == 0, "hand-off wait timed out"
+    again = [torch.full_like(q, float("nan")) for _ in range(3)]
+    k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *again, D ** -0.5, 1 - (variant & 1))
+    torch.cuda.synchronize()
+    for a, b in zip(got, again):
+        assert torch.equal(a, b)
+    monkeypatch.setenv("OWLK_BWD_FUSED", "0")
+    split = [torch.empty_like(q) for _ in range(3)]
+    k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, *split)
+    qr, kr, vr = (t.cpu().float().view(B, L, H, D).transpose(1, 2).requires_grad_() for t in (q, kk, v))
+    m = R.frame_mask(L, L, tpf, window, doc, causal=True)
+    oref = R.attention(qr, kr, vr, m)
+    oref.backward(do.cpu().float().view(B, L, H, D).transpose(1, 2))
+    for name, g, s, ref in zip(("dq", "dk", "dv"), got, split, (qr.grad, kr.grad, vr.grad)):
+        assert torch.isfinite(g).all(), name
+        assert rel(g.view(B, L, H, D).transpose(1, 2), ref) < 1e-2, name
+        assert rel(g, s) < 5e-3, name

@@ -894,8 +894,11 @@ def test_attention_packed_runs_match_general_doc_path(case, D):
         dq, dk, dv = (torch.empty_like(q) for _ in range(3))
         k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, dq, dk, dv)
         res.append((o, lse, dq, dk, dv))
-    for a, b in zip(*res):
-        assert rel(a, b) < 1e-5
+    # D = 64: the runs form's backward is the single pass (attn_bwd_fused.hip), whose dQ / dK / dV
+    # differ from the two-kernel path's in fp32 summation order and the bf16 dS of the dQ product
+    fused = k.fused_bwd_variant(D, k.FrameMask(tpf, window, True, 0, arrays)) is not None
+    for i, (a, b) in enumerate(zip(*res)):
+        assert rel(a, b) < (5e-3 if fused and i >= 2 else 1e-5)
     ref = R.attention(*(t.cpu().float().view(B, L, H, D).transpose(1, 2) for t in (q, kk, v)),
                       R.frame_mask(L, L, tpf, window, doc))
     assert rel(res[0][0].view(B, L, H, D).transpose(1, 2), ref) < 1e-2
