@@ -73,7 +73,7 @@
 #define OWLK_FUSED_DEQ_PF 1
 #endif
 #ifndef OWLK_FUSED_DQ_PF
-#define OWLK_FUSED_DQ_PF 2
+#define OWLK_FUSED_DQ_PF 3
 #endif
 
 namespace {
