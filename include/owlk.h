@@ -103,23 +103,29 @@ int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const voi
 
 /* ---- QK RMSNorm + RoPE (attn.py:83-89, rope.py:43-51): qkv rows [q(h d)|k(h d)|v(h d)] ->
  *   out rows [rope(bf16(rms(q)))|rope(bf16(rms(k)))], rotation pairs (2i, 2i+1) written to
- *   (i, D/2 + i); cos/sin fp32 tables [*, D/2] at row tab_off + (tpos_div ? t % tpos_div : t). */
+ *   (i, D/2 + i); cos/sin fp32 tables [n_tab, D/2] (row stride ld_tab) at row
+ *   tab_off + (tpos_div ? t % tpos_div : t).  Every row read must lie in the table (else returns 1:
+ *   the reference's cos[offset:offset + n] slice comes out short and its rotation fails, rope.py:46-49). */
 int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const float* cosb, const float* sinb,
-                     long ld_tab, long tab_off, long tpos_div, void* out, long ldo, float* rstd, void* stream);
+                     long ld_tab, long n_tab, long tab_off, long tpos_div, void* out, long ldo, float* rstd,
+                     void* stream);
 /* decode form (attn.py:86-104 cache branch): q and k rotated as above, v copied, each into its own
  * destination (row stride ld*, batch stride s*; token t -> batch t / L, row t % L): k and v go
  * straight into the KV cache behind its window; no rstd */
 int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
-                        const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
-                        long ldko, long sko, void* vo, long ldvo, long svo, void* stream);
+                        const float* sinb, long ld_tab, long n_tab, long tab_off, void* qo, long ldqo, long sqo,
+                        void* ko, long ldko, long sko, void* vo, long ldvo, long svo, void* stream);
 /* the same with the cache position on the device: state = {start, cached tokens, rope offset}
- * (int64), k / v written to rows start + cached + t of kbuf / vbuf, rope position offset + t; one
- * captured HIP graph then serves every frame of a growing cache */
+ * (int64), k / v written to rows start + cached + t of kbuf / vbuf ([B, cap, H D]), rope position
+ * offset + t; one captured HIP graph then serves every frame of a growing cache.  A state whose rows
+ * fall outside the cap buffer rows or the n_tab table rows is not followed: the kernel writes NaN q
+ * rows and touches neither the cache nor the table. */
 int owlk_qk_rope_fwd_kv_dev(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
-                            const float* sinb, long ld_tab, const long* state, void* qo, long ldqo, long sqo,
-                            void* kbuf, long ldk, long skb, void* vbuf, long ldv, long svb, void* stream);
+                            const float* sinb, long ld_tab, long n_tab, const long* state, void* qo, long ldqo,
+                            long sqo, void* kbuf, long ldk, long skb, void* vbuf, long ldv, long svb, long cap,
+                            void* stream);
 int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
-                     const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
+                     const float* cosb, const float* sinb, long ld_tab, long n_tab, long tab_off, long tpos_div,
                      const float* rstd, void* dqkv, long ldg, void* stream);
 /* owlk_qk_rope_bwd with the column sums of its output fused: dbias[n] += sum_t bf16(dqkv[t, n]) for
  * n < 2 H D -- the q / k part of the qkv Linear's bias gradient (attn.py:90; torch's Linear backward
@@ -127,7 +133,7 @@ int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long 
  * owlk_qk_rope_bwd_ws_bytes; 0 = shape not supported by the fused form), added in a fixed order. */
 long owlk_qk_rope_bwd_ws_bytes(long T, int H, int D);
 int owlk_qk_rope_bwd_bias(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
-                          const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
+                          const float* cosb, const float* sinb, long ld_tab, long n_tab, long tab_off, long tpos_div,
                           const float* rstd, void* dqkv, long ldg, float* dbias, void* ws, long ws_bytes,
                           void* stream);
 
@@ -152,14 +158,14 @@ int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, long ldk, lo
                   void* stream);
 /* Decode attention (attn.py:86-107 cache branch) with the cache position on the device: one frame
  * of Lq <= 64 queries per (batch, head), unmasked over [cache | Lnew new rows] of the cache
- * buffers kbuf / vbuf (the new rows written there first, owlk_qk_rope_fwd_kv_dev), or over the
- * last window_tokens of them (windowed layer; 0: all); state = {start, cached tokens, rope offset}
- * int64 on the device.  head_dim 64 or 128, bounded softmax (score_bound > 0) only; lse base 2 as
- * owlk_attn_fwd's. */
+ * buffers kbuf / vbuf ([B, cap, H D]; the new rows written there first, owlk_qk_rope_fwd_kv_dev), or
+ * over the last window_tokens of them (windowed layer; 0: all); state = {start, cached tokens, rope
+ * offset} int64 on the device (rows past cap: NaN output, nothing read).  head_dim 64 or 128,
+ * bounded softmax (score_bound > 0) only; lse base 2 as owlk_attn_fwd's. */
 int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const void* kbuf, long ldk, long skb,
                          const void* vbuf, long ldv, long svb, void* o, long ldo, long sob, float* lse, long B,
                          int H, long Lq, int head_dim, float scale, float score_bound, const long* state,
-                         long Lnew, long window_tokens, void* stream);
+                         long Lnew, long window_tokens, long cap, void* stream);
 /* delta[b, h, t] = sum_d dO * O (fp32), the backward's row constant */
 int owlk_attn_delta(const void* o, const void* dout, long ld, long B, long L, int H, int D, float* delta,
                     void* stream);

@@ -807,12 +807,29 @@ struct DecCfg {
 
 template <int D>
 __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long* __restrict__ state, long Lnew,
-                                                             long wtok) {
+                                                             long wtok, long cap) {
   // device-resident cache state (owlk_attn_decode_fwd): {start, cached tokens, rope offset} of the
   // cache buffers p.k / p.v, so one captured HIP graph serves every frame of a growing cache; the
   // keys are [cache | the Lnew new rows], the last wtok of them for a windowed layer (wtok > 0)
   if (state) {
     const long start = state[0], total = state[1] + Lnew;
+    if (start < 0 || state[1] < 0 || start + total > cap) {
+      // a window past the cap rows of the buffers: read nothing, NaN rows out (the host checks
+      // every position it sets; this guards a replayed graph)
+      const long b = blockIdx.z;
+      const int head = blockIdx.y;
+      constexpr int DQ = D / 4;
+      const int q = threadIdx.x >> 2, d0 = DQ * (threadIdx.x & 3);
+      if (q >= p.Lq) return;
+      bf16* O = p.o + b * p.sob + (long)q * p.ldo + head * D + d0;
+      bf16x8 nan8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nan8[e] = (bf16)NAN;
+#pragma unroll
+      for (int h8 = 0; h8 < DQ / 8; ++h8) *(bf16x8*)(O + 8 * h8) = nan8;
+      if ((threadIdx.x & 3) == 0) p.lse[(b * p.H + head) * p.Lq + q] = NAN;
+      return;
+    }
     const long first = wtok > 0 && total > wtok ? total - wtok : 0;
     p.k += (start + first) * p.ldk;
     p.v += (start + first) * p.ldv;
@@ -989,7 +1006,7 @@ void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
   if (split && p.bound > 0.f && p.Lq <= 64 && p.Lkv >= 4 * KT && m.window == 0 && !m.causal && !m.kv_lo &&
       !m.doc && m.q_offset == 0) {
     hipLaunchKernelGGL(attn_fwd16_split_k<D>, dim3(1, grid.y, grid.z), dim3(256), 0, s, p, (const long*)nullptr,
-                       0L, 0L);
+                       0L, 0L, 0L);
     return;
   }
   // D 128: the 16x16x32 form with 32 queries per wave (OWLK_FWD16_128=0: the 32x32x16 attn_fwd_k)
@@ -1085,9 +1102,10 @@ extern "C" int owlk_attn_fwd(const void* q, long ldq, long sqb, const void* k, l
 extern "C" int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const void* kbuf, long ldk, long skb,
                                     const void* vbuf, long ldv, long svb, void* o, long ldo, long sob, float* lse,
                                     long B, int H, long Lq, int head_dim, float scale, float score_bound,
-                                    const long* state, long Lnew, long window_tokens, void* stream) {
+                                    const long* state, long Lnew, long window_tokens, long cap, void* stream) {
   OWLK_REQUIRE(head_dim == 64 || head_dim == 128, "attn_decode_fwd: head_dim %d not built (64, 128)", head_dim);
   OWLK_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lq <= 64 && Lnew > 0 && state, "attn_decode_fwd: bad sizes");
+  OWLK_REQUIRE(cap >= Lnew, "attn_decode_fwd: cache capacity %ld rows", cap);
   OWLK_REQUIRE(score_bound > 0.f && score_bound * scale < 40.f, "attn_decode_fwd: needs a score bound");
   OWLK_REQUIRE(((uintptr_t)q | (uintptr_t)kbuf | (uintptr_t)vbuf | (uintptr_t)o) % 16 == 0 && ldq % 8 == 0 &&
                    ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0,
@@ -1102,9 +1120,9 @@ extern "C" int owlk_attn_decode_fwd(const void* q, long ldq, long sqb, const voi
   p.m = owlk_make_mask(1, 0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, 0);
   if (head_dim == 64)
     hipLaunchKernelGGL(attn_fwd16_split_k<64>, dim3(1, (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
-                       p, state, Lnew, window_tokens);
+                       p, state, Lnew, window_tokens, cap);
   else
     hipLaunchKernelGGL(attn_fwd16_split_k<128>, dim3(1, (unsigned)H, (unsigned)B), dim3(256), 0, (hipStream_t)stream,
-                       p, state, Lnew, window_tokens);
+                       p, state, Lnew, window_tokens, cap);
   return owlk::check_launch("attn_decode_fwd");
 }

@@ -328,13 +328,7 @@ __global__ __launch_bounds__(256) void qk_rope_kv_k(const bf16* __restrict__ qkv
                                                     long ld_tab, long tab_off, bf16* __restrict__ qo, long ldqo,
                                                     long sqo, bf16* __restrict__ ko, long ldko, long sko,
                                                     bf16* __restrict__ vo, long ldvo, long svo,
-                                                    const long* __restrict__ state) {
-  if (state) {  // {start, cached tokens, rope offset}: k / v rows go behind the window of the buffers
-    const long row0 = state[0] + state[1];
-    ko += row0 * ldko;
-    vo += row0 * ldvo;
-    tab_off = state[2];
-  }
+                                                    const long* __restrict__ state, long n_tab, long cap) {
   constexpr int CPR = D / 8;
   const long gid = (long)blockIdx.x * 256 + threadIdx.x;
   const long rowid = gid / CPR;  // (token, which, head)
@@ -343,6 +337,23 @@ __global__ __launch_bounds__(256) void qk_rope_kv_k(const bf16* __restrict__ qkv
   const long tok = rowid / (3 * H);
   const int wh = rowid % (3 * H);  // which * H + head
   const long bb = tok / L, t = tok - bb * L;
+  if (state) {  // {start, cached tokens, rope offset}: k / v rows go behind the window of the buffers
+    const long start = state[0], cached = state[1], off = state[2];
+    if (start < 0 || cached < 0 || start + cached + L > cap || off < 0 || off + L > n_tab) {
+      // a position past the cache buffers or the rope table (the host checks every position it
+      // sets; this guards the replayed graph): touch neither, poison this row of q with NaN
+      if (wh < H) {
+        const bf16x4 nan4 = {(bf16)NAN, (bf16)NAN, (bf16)NAN, (bf16)NAN};
+        bf16* o = qo + bb * sqo + t * ldqo + (long)wh * D;
+        *(bf16x4*)(o + j * 4) = nan4;
+        *(bf16x4*)(o + D / 2 + j * 4) = nan4;
+      }
+      return;
+    }
+    ko += (start + cached) * ldko;
+    vo += (start + cached) * ldvo;
+    tab_off = off;
+  }
   const bf16x8 v = *(const bf16x8*)(qkv + tok * ldq + (long)wh * D + j * 8);
   if (wh >= 2 * H) {  // v: copied as is
     *(bf16x8*)(vo + bb * svo + t * ldvo + (long)(wh - 2 * H) * D + j * 8) = v;
@@ -742,10 +753,20 @@ extern "C" int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy
   return owlk::check_launch("gate_bwd");
 }
 
+// every table row a launch reads lies inside the [n_tab, ld_tab] cos / sin tables (the reference
+// slices cos[offset:offset + n] and fails on a short slice, rope.py:46-49; a kernel would read past
+// the buffer instead)
+static bool rope_rows_ok(long T, long n_tab, long tab_off, long tpos_div) {
+  const long span = tpos_div > 0 ? (T < tpos_div ? T : tpos_div) : T;
+  return n_tab > 0 && tab_off >= 0 && tab_off + span <= n_tab;
+}
+
 extern "C" int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const float* cosb,
-                                const float* sinb, long ld_tab, long tab_off, long tpos_div, void* out, long ldo,
-                                float* rstd, void* stream) {
+                                const float* sinb, long ld_tab, long n_tab, long tab_off, long tpos_div, void* out,
+                                long ldo, float* rstd, void* stream) {
   OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_fwd: head_dim %d unsupported", D);
+  OWLK_REQUIRE(rope_rows_ok(T, n_tab, tab_off, tpos_div), "qk_rope_fwd: positions %ld.. past the %ld-row rope table",
+               tab_off, n_tab);
   const long threads = T * 2 * H * (D / 8);
   dim3 g((unsigned)((threads + 255) / 256));
   if (D == 64)
@@ -758,28 +779,35 @@ extern "C" int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D,
 }
 
 static int qk_rope_kv_launch(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
-                             const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
-                             long ldko, long sko, void* vo, long ldvo, long svo, const long* state, void* stream);
+                             const float* sinb, long ld_tab, long n_tab, long tab_off, void* qo, long ldqo, long sqo,
+                             void* ko, long ldko, long sko, void* vo, long ldvo, long svo, const long* state,
+                             long cap, void* stream);
+
 
 extern "C" int owlk_qk_rope_fwd_kv(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
-                                   const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo,
-                                   void* ko, long ldko, long sko, void* vo, long ldvo, long svo, void* stream) {
-  return qk_rope_kv_launch(qkv, ldq, T, L, H, D, cosb, sinb, ld_tab, tab_off, qo, ldqo, sqo, ko, ldko, sko, vo, ldvo,
-                           svo, nullptr, stream);
+                                   const float* sinb, long ld_tab, long n_tab, long tab_off, void* qo, long ldqo,
+                                   long sqo, void* ko, long ldko, long sko, void* vo, long ldvo, long svo,
+                                   void* stream) {
+  OWLK_REQUIRE(L > 0 && rope_rows_ok(L, n_tab, tab_off, 0), "qk_rope_fwd_kv: positions %ld.. past the %ld-row rope table",
+               tab_off, n_tab);
+  return qk_rope_kv_launch(qkv, ldq, T, L, H, D, cosb, sinb, ld_tab, n_tab, tab_off, qo, ldqo, sqo, ko, ldko, sko, vo,
+                           ldvo, svo, nullptr, 0, stream);
 }
 
 extern "C" int owlk_qk_rope_fwd_kv_dev(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
-                                       const float* sinb, long ld_tab, const long* state, void* qo, long ldqo,
-                                       long sqo, void* kbuf, long ldk, long skb, void* vbuf, long ldv, long svb,
-                                       void* stream) {
+                                       const float* sinb, long ld_tab, long n_tab, const long* state, void* qo,
+                                       long ldqo, long sqo, void* kbuf, long ldk, long skb, void* vbuf, long ldv,
+                                       long svb, long cap, void* stream) {
   OWLK_REQUIRE(state, "qk_rope_fwd_kv_dev: state pointer required");
-  return qk_rope_kv_launch(qkv, ldq, T, L, H, D, cosb, sinb, ld_tab, 0, qo, ldqo, sqo, kbuf, ldk, skb, vbuf, ldv, svb,
-                           state, stream);
+  OWLK_REQUIRE(n_tab > 0 && cap > 0, "qk_rope_fwd_kv_dev: rope table rows / cache capacity required");
+  return qk_rope_kv_launch(qkv, ldq, T, L, H, D, cosb, sinb, ld_tab, n_tab, 0, qo, ldqo, sqo, kbuf, ldk, skb, vbuf, ldv,
+                           svb, state, cap, stream);
 }
 
 static int qk_rope_kv_launch(const void* qkv, long ldq, long T, long L, int H, int D, const float* cosb,
-                             const float* sinb, long ld_tab, long tab_off, void* qo, long ldqo, long sqo, void* ko,
-                             long ldko, long sko, void* vo, long ldvo, long svo, const long* state, void* stream) {
+                             const float* sinb, long ld_tab, long n_tab, long tab_off, void* qo, long ldqo, long sqo,
+                             void* ko, long ldko, long sko, void* vo, long ldvo, long svo, const long* state,
+                             long cap, void* stream) {
   OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_fwd_kv: head_dim %d unsupported", D);
   OWLK_REQUIRE(L > 0 && T % L == 0, "qk_rope_fwd_kv: T=%ld is not a whole number of L=%ld rows", T, L);
   OWLK_REQUIRE(((uintptr_t)qo | (uintptr_t)ko | (uintptr_t)vo) % 16 == 0 && ldqo % 8 == 0 && ldko % 8 == 0 &&
@@ -789,17 +817,21 @@ static int qk_rope_kv_launch(const void* qkv, long ldq, long T, long L, int H, i
   dim3 g((unsigned)((threads + 255) / 256));
   if (D == 64)
     hipLaunchKernelGGL(qk_rope_kv_k<64>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, L, H, cosb,
-                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo, state);
+                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo, state,
+                       n_tab, cap);
   else
     hipLaunchKernelGGL(qk_rope_kv_k<128>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ldq, T, L, H, cosb,
-                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo, state);
+                       sinb, ld_tab, tab_off, (bf16*)qo, ldqo, sqo, (bf16*)ko, ldko, sko, (bf16*)vo, ldvo, svo, state,
+                       n_tab, cap);
   return owlk::check_launch("qk_rope_fwd_kv");
 }
 
 extern "C" int owlk_qk_rope_bwd(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
-                                const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
-                                const float* rstd, void* dqkv, long ldg, void* stream) {
+                                const float* cosb, const float* sinb, long ld_tab, long n_tab, long tab_off,
+                                long tpos_div, const float* rstd, void* dqkv, long ldg, void* stream) {
   OWLK_REQUIRE(D == 64 || D == 128, "qk_rope_bwd: head_dim %d unsupported", D);
+  OWLK_REQUIRE(rope_rows_ok(T, n_tab, tab_off, tpos_div), "qk_rope_bwd: positions %ld.. past the %ld-row rope table",
+               tab_off, n_tab);
   const long threads = T * 2 * H * (D / 8);
   dim3 g((unsigned)((threads + 255) / 256));
   if (D == 64)
@@ -828,9 +860,11 @@ extern "C" long owlk_qk_rope_bwd_ws_bytes(long T, int H, int D) {
 }
 
 extern "C" int owlk_qk_rope_bwd_bias(const void* dqk, long ldd, const void* qkv, long ldq, long T, int H, int D,
-                                     const float* cosb, const float* sinb, long ld_tab, long tab_off, long tpos_div,
-                                     const float* rstd, void* dqkv, long ldg, float* dbias, void* ws, long ws_bytes,
-                                     void* stream) {
+                                     const float* cosb, const float* sinb, long ld_tab, long n_tab, long tab_off,
+                                     long tpos_div, const float* rstd, void* dqkv, long ldg, float* dbias, void* ws,
+                                     long ws_bytes, void* stream) {
+  OWLK_REQUIRE(rope_rows_ok(T, n_tab, tab_off, tpos_div),
+               "qk_rope_bwd_bias: positions %ld.. past the %ld-row rope table", tab_off, n_tab);
   long rows_per = 0;
   const long nb = qk_rope_bwd_blocks(T, H, D, &rows_per);
   const long N = 2L * H * D;

@@ -28,13 +28,13 @@ _SIGS = {
     "owlk_cond_silu_fwd": [P, P, P, P, L, L, I, P, P, P],
     "owlk_cond_silu_bwd": [P, I, P, P, L, L, I, P, P, P],
     "owlk_small_k_wgrad": [P, L, P, L, L, L, I, P, L, F, P],
-    "owlk_qk_rope_fwd": [P, L, L, I, I, P, P, L, L, L, P, L, P, P],
-    "owlk_qk_rope_fwd_kv": [P, L, L, L, I, I, P, P, L, L, P, L, L, P, L, L, P, L, L, P],
-    "owlk_qk_rope_fwd_kv_dev": [P, L, L, L, I, I, P, P, L, P, P, L, L, P, L, L, P, L, L, P],
-    "owlk_attn_decode_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, I, F, F, P, L, L, P],
-    "owlk_qk_rope_bwd": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P],
+    "owlk_qk_rope_fwd": [P, L, L, I, I, P, P, L, L, L, L, P, L, P, P],
+    "owlk_qk_rope_fwd_kv": [P, L, L, L, I, I, P, P, L, L, L, P, L, L, P, L, L, P, L, L, P],
+    "owlk_qk_rope_fwd_kv_dev": [P, L, L, L, I, I, P, P, L, L, P, P, L, L, P, L, L, P, L, L, L, P],
+    "owlk_attn_decode_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, I, F, F, P, L, L, L, P],
+    "owlk_qk_rope_bwd": [P, L, P, L, L, I, I, P, P, L, L, L, L, P, P, L, P],
     "owlk_qk_rope_bwd_ws_bytes": [L, I, I],
-    "owlk_qk_rope_bwd_bias": [P, L, P, L, L, I, I, P, P, L, L, L, P, P, L, P, P, L, P],
+    "owlk_qk_rope_bwd_bias": [P, L, P, L, L, I, I, P, P, L, L, L, L, P, P, L, P, P, L, P],
     "owlk_attn_fwd": [P, L, L, P, L, L, P, L, L, P, L, L, P, L, I, L, L, I, F, F, L, I, I, L, P, P, P, P, L, P],
     "owlk_attn_delta": [P, P, L, L, L, I, I, P, P],
     "owlk_frame_mux": [I, L, I, I, I, P, L, P, L, P, L, P],

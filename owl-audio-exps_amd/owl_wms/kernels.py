@@ -256,8 +256,8 @@ def qk_rope_fwd(qkv, H, D, cos, sin, tab_off=0, tpos_div=0):
     T = qkv.shape[0]
     out = torch.empty(T, 2 * H * D, device=qkv.device, dtype=BF16)
     rstd = torch.empty(T, 2 * H, device=qkv.device, dtype=F32)
-    call("owlk_qk_rope_fwd", ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin), cos.stride(0), tab_off, tpos_div,
-         ptr(out), out.stride(0), ptr(rstd), stream())
+    call("owlk_qk_rope_fwd", ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin), cos.stride(0), cos.shape[0],
+         tab_off, tpos_div, ptr(out), out.stride(0), ptr(rstd), stream())
     return out, rstd
 
 
@@ -266,8 +266,8 @@ def qk_rope_fwd_kv(qkv, B, L, H, D, cos, sin, tab_off, q_out, k_out, v_out):
     v copied into v_out (views of the KV cache's slots; any row / batch strides)."""
     for t, nm in ((q_out, "q_out"), (k_out, "k_out"), (v_out, "v_out")):
         assert t.shape == (B, L, H * D) and t.stride(2) == 1 and t.dtype == BF16, nm
-    call("owlk_qk_rope_fwd_kv", ptr(qkv), qkv.stride(0), B * L, L, H, D, ptr(cos), ptr(sin), cos.stride(0), tab_off,
-         ptr(q_out), q_out.stride(1), q_out.stride(0), ptr(k_out), k_out.stride(1), k_out.stride(0),
+    call("owlk_qk_rope_fwd_kv", ptr(qkv), qkv.stride(0), B * L, L, H, D, ptr(cos), ptr(sin), cos.stride(0),
+         cos.shape[0], tab_off, ptr(q_out), q_out.stride(1), q_out.stride(0), ptr(k_out), k_out.stride(1), k_out.stride(0),
          ptr(v_out), v_out.stride(1), v_out.stride(0), stream())
 
 
@@ -278,9 +278,10 @@ def qk_rope_fwd_kv_dev(qkv, B, L, H, D, cos, sin, state, q_out, kbuf, vbuf):
     assert q_out.shape == (B, L, H * D) and q_out.stride(2) == 1
     for t in (kbuf, vbuf):
         assert t.dim() == 3 and t.shape[0] == B and t.shape[2] == H * D and t.stride(2) == 1 and t.dtype == BF16
+    assert kbuf.shape[1] == vbuf.shape[1]
     call("owlk_qk_rope_fwd_kv_dev", ptr(qkv), qkv.stride(0), B * L, L, H, D, ptr(cos), ptr(sin), cos.stride(0),
-         ptr(state), ptr(q_out), q_out.stride(1), q_out.stride(0), ptr(kbuf), kbuf.stride(1), kbuf.stride(0),
-         ptr(vbuf), vbuf.stride(1), vbuf.stride(0), stream())
+         cos.shape[0], ptr(state), ptr(q_out), q_out.stride(1), q_out.stride(0), ptr(kbuf), kbuf.stride(1),
+         kbuf.stride(0), ptr(vbuf), vbuf.stride(1), vbuf.stride(0), kbuf.shape[1], stream())
 
 
 def decode_dev_supported(D, L):
@@ -299,7 +300,7 @@ def attn_decode_fwd(q, kbuf, vbuf, H, D, state, Lnew, window_tokens=0, scale=Non
     call("owlk_attn_decode_fwd", ptr(q), q.stride(1), q.stride(0), ptr(kbuf), kbuf.stride(1), kbuf.stride(0),
          ptr(vbuf), vbuf.stride(1), vbuf.stride(0), ptr(o), o.stride(1), o.stride(0), ptr(lse), B, H, Lq, D,
          float(scale if scale is not None else D ** -0.5), float(score_bound), ptr(state), Lnew, window_tokens,
-         stream())
+         min(kbuf.shape[1], vbuf.shape[1]), stream())
     return o, lse
 
 
@@ -307,8 +308,8 @@ def qk_rope_bwd(dqk, qkv, rstd, H, D, cos, sin, dqkv, tab_off=0, tpos_div=0, dbi
     """-> dqkv[:, :2HD]; with dbias (fp32 [2HD]) also dbias += column sums of those outputs (the q / k
     part of the qkv bias gradient), fused into the same pass where the shape allows."""
     T = qkv.shape[0]
-    args = (ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin), cos.stride(0), tab_off,
-            tpos_div, ptr(rstd), ptr(dqkv), dqkv.stride(0))
+    args = (ptr(dqk), dqk.stride(0), ptr(qkv), qkv.stride(0), T, H, D, ptr(cos), ptr(sin), cos.stride(0),
+            cos.shape[0], tab_off, tpos_div, ptr(rstd), ptr(dqkv), dqkv.stride(0))
     nb = lib().owlk_qk_rope_bwd_ws_bytes(T, H, D) if dbias is not None else 0
     if nb > 0:
         assert dbias.dtype == F32 and dbias.is_contiguous() and dbias.numel() == 2 * H * D

@@ -65,6 +65,16 @@ def _single_document(doc_id, n_frames):
     return res
 
 
+def check_rope_rows(rope, offset, n):
+    """Positions offset .. offset + n - 1 must lie in the RoPE table (config.n_frames frames): the
+    reference slices cos[offset:offset + n] and its rotation fails on the short slice (rope.py:46-49);
+    the kernels would read past the table instead, so this raises first, as the reference does."""
+    rows = rope.cos.shape[0]
+    if offset < 0 or offset + n > rows:
+        raise RuntimeError(f"RoPE positions {offset}..{offset + n - 1} lie past the {rows}-row table "
+                           f"(config.n_frames frames); decode at most n_frames frames of context + new frames")
+
+
 class Attn(nn.Module):
     def __init__(self, config, layer_idx, local=False, rope=None):
         super().__init__()
@@ -94,6 +104,7 @@ class Attn(nn.Module):
         H = self.n_heads
         D = d // H
         offset = kv_cache.get_offset(self.layer_idx) if kv_cache is not None else 0
+        check_rope_rows(self.rope, offset, L)
         if block_mask is None and getattr(kv_cache, "dev", None) is not None and offset > 0 and \
                 K.decode_dev_supported(D, L):
             # decode with the cache position on the device (one captured graph for every frame)

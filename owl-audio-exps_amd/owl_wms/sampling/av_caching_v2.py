@@ -16,8 +16,16 @@ the keys the reference's forward sees.
 import torch
 
 from .. import kernels as K
+from ..nn.attn import check_rope_rows
 from ..nn.kv_cache import KVCache
 from .schedulers import get_deltas, get_sd3_euler
+
+
+def _release_graph(g):
+    """Destroy a step graph only after its queued replays have run: its exec (kernel arguments) and
+    its private memory pool are released here, so no replay of it may still be queued then."""
+    torch.cuda.current_stream().synchronize()
+    g.reset()
 
 
 class AVCachingSamplerV2:
@@ -82,8 +90,9 @@ class AVCachingSamplerV2:
         for t_idx in range(first, self.n_steps):
             sdt.copy_(dt[t_idx])
             g.replay()
-        del g
-        return sx.clone(), st.clone()
+        out = sx.clone(), st.clone()
+        _release_graph(g)
+        return out
 
     def _euler_replay(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
         """compile_on_decode with the cache position on the device (SingleKVCache.enable_device_state):
@@ -116,6 +125,11 @@ class AVCachingSamplerV2:
             first = 1
         else:
             g, bufs = st
+            # the replayed step reads its positions from the device: check them here as the eager
+            # step's Attn._attend does (the kernels would only poison the rows with NaN)
+            rope = getattr(model.transformer, "rope", None)
+            if rope is not None:
+                check_rope_rows(rope, kv_cache.get_offset(0), model.config.tokens_per_frame)
             for k, v in (("x", x), ("t", t), ("mouse", mouse), ("btn", btn)):
                 bufs[k].copy_(v)
         g, bufs = st
@@ -184,5 +198,7 @@ class AVCachingSamplerV2:
                     kv_cache.truncate(1, front=False)
         finally:
             model.transformer.disable_decoding()
+            if self._step_graph is not None:
+                _release_graph(self._step_graph[0])
             self._step_graph = None
         return torch.cat(latents, dim=1)

@@ -380,6 +380,60 @@ def test_attention_decode_device_state(D, Lq, start, cached, window):
     assert (lse - lse_ref).abs().max().item() < 4e-3
 
 
+@pytest.mark.parametrize("D", [64, 128])
+def test_decode_positions_are_bounded(D):
+    """Every position a rope / decode kernel follows is bounded by the RoPE table rows and the cache
+    capacity (round 4's illegal-address fault, profiles/r4ac_gemm_nowait_tests_fault.log, was a decode
+    test running past the table: the rope kernels read 64 rows beyond it).  Host-given positions past
+    the table raise (the reference's short cos slice fails, rope.py:46-49); a device state past them
+    (a replayed graph) leaves the cache buffers untouched, reads nothing and poisons its outputs with
+    NaN; in range, exactly rows start + cached .. + L are written, as the host-position form writes."""
+    k = K()
+    B, H, L, cap = 2, 2, 64, 256
+    ang = R.motion_rope_angles(3, 8, D)  # 3 frames x 64 tokens = 192 table rows
+    rows = ang.shape[0]
+    cos, sin = ang.cos().to(DEV), ang.sin().to(DEV)
+    qkv = rnd(B * L, 3 * H * D, seed=90)
+    with pytest.raises(RuntimeError, match="rope table"):
+        k.qk_rope_fwd(qkv, H, D, cos, sin, rows - L + 1, L)
+    with pytest.raises(RuntimeError, match="rope table"):
+        k.qk_rope_fwd(qkv, H, D, cos, sin, 0, 0)  # T = B L rows from row 0: past the table
+    with pytest.raises(RuntimeError, match="rope table"):
+        k.qk_rope_bwd(qkv[:, :2 * H * D].contiguous(), qkv, torch.ones(B * L, 2 * H, device=DEV), H, D, cos, sin,
+                      torch.empty_like(qkv), rows - L + 1, L)
+    kb, vb = rnd(B, cap, H * D, seed=91), rnd(B, cap, H * D, seed=92)
+    qbuf = torch.empty(B, L, H * D, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="rope table"):
+        k.qk_rope_fwd_kv(qkv, B, L, H, D, cos, sin, rows - L + 1, qbuf, kb[:, :L], vb[:, :L])
+    k0, v0 = kb.clone(), vb.clone()
+    for st in ([0, cap - L + 1, 0, 0], [cap, 0, 0, 0], [-64, 0, 0, 0], [0, 0, rows - L + 1, 0], [0, 0, -1, 0]):
+        state = torch.tensor(st, dtype=torch.int64, device=DEV)
+        q = torch.zeros(B, L, H * D, device=DEV, dtype=torch.bfloat16)
+        k.qk_rope_fwd_kv_dev(qkv, B, L, H, D, cos, sin, state, q, kb, vb)
+        torch.cuda.synchronize()
+        assert torch.equal(kb, k0) and torch.equal(vb, v0), st
+        assert torch.isnan(q.float()).all(), st
+    # in range (last table rows, last cache rows): the host-position form's result, nothing else written
+    start, cached = 16, cap - L - 16
+    state = torch.tensor([start, cached, rows - L, 0], dtype=torch.int64, device=DEV)
+    q = torch.empty(B, L, H * D, device=DEV, dtype=torch.bfloat16)
+    k.qk_rope_fwd_kv_dev(qkv, B, L, H, D, cos, sin, state, q, kb, vb)
+    qr, kr, vr = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    k.qk_rope_fwd_kv(qkv, B, L, H, D, cos, sin, rows - L, qr, kr, vr)
+    r0 = start + cached
+    assert torch.equal(q, qr) and torch.equal(kb[:, r0:], kr) and torch.equal(vb[:, r0:], vr)
+    assert torch.equal(kb[:, :r0], k0[:, :r0]) and torch.equal(vb[:, :r0], v0[:, :r0])
+    # decode attention over a window past the buffers: NaN rows, nothing read
+    for st in ([0, cap, 0, 0], [cap - L, 1, 0, 0], [-1, 0, 0, 0]):
+        state = torch.tensor(st, dtype=torch.int64, device=DEV)
+        o, lse = k.attn_decode_fwd(qr, kb, vb, H, D, state, L, 0, score_bound=k.qk_norm_bound(D))
+        torch.cuda.synchronize()
+        assert torch.isnan(o.float()).all() and torch.isnan(lse).all(), st
+    state = torch.tensor([start, cached, 0, 0], dtype=torch.int64, device=DEV)
+    o, _ = k.attn_decode_fwd(qr, kb, vb, H, D, state, L, 0, score_bound=k.qk_norm_bound(D))
+    assert torch.isfinite(o.float()).all()
+
+
 @pytest.mark.parametrize("D,window", [(64, None), (64, 2), (128, None)])
 def test_integration_binding_lse_contract(D, window):
     """The reference-side binding of INTEGRATION.md (owlk_bind.attn_fwd) run against the real

@@ -558,9 +558,12 @@ def test_device_state_decode_matches_host_state(d_model):
     from owl_wms.sampling import get_sampler_cls
     m = _model(d_model).eval()
     g = torch.Generator().manual_seed(7)
-    x = torch.randn(2, 4, 32, 8, 8, generator=g).bfloat16().cuda()
-    mouse = torch.randn(2, 9, 2, generator=g).bfloat16().cuda()
-    btn = (torch.rand(2, 9, 11, generator=g) < 0.5).bfloat16().cuda()
+    # 3 context + 5 new frames = the model's n_frames (8): every RoPE position lies in the table
+    # (round 4 ran 4 + 5 here, past the table: the rope kernels read 64 rows beyond it, which is
+    # what faulted in profiles/r4ac_gemm_nowait_tests_fault.log; such calls now raise)
+    x = torch.randn(2, 3, 32, 8, 8, generator=g).bfloat16().cuda()
+    mouse = torch.randn(2, 8, 2, generator=g).bfloat16().cuda()
+    btn = (torch.rand(2, 8, 11, generator=g) < 0.5).bfloat16().cuda()
     outs = []
     for dev in (False, True):
         torch.manual_seed(321)
@@ -569,6 +572,25 @@ def test_device_state_decode_matches_host_state(d_model):
         outs.append(s(m.core, x, mouse, btn).float())
     assert rel(outs[1], outs[0]) < 2e-2
     assert torch.isfinite(outs[1]).all()
+
+
+@pytest.mark.parametrize("device_state,graphed", [(False, False), (True, False), (True, True)])
+def test_decode_past_rope_table_raises(device_state, graphed):
+    """Decoding past config.n_frames frames: the reference's rope slices cos[offset:offset + n] short
+    and its rotation fails (rope.py:46-49); this path raises before any kernel reads past the table
+    (4 context + 5 new frames with n_frames 8), on the eager, device-state and replayed paths, and the
+    GPU is left healthy (the sync below)."""
+    from owl_wms.sampling import get_sampler_cls
+    m = _model(128).eval()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(1, 4, 32, 8, 8, generator=g).bfloat16().cuda()
+    mouse = torch.randn(1, 9, 2, generator=g).bfloat16().cuda()
+    btn = (torch.rand(1, 9, 11, generator=g) < 0.5).bfloat16().cuda()
+    s = get_sampler_cls("av_caching")(n_steps=2, cfg_scale=1.3, num_frames=5, noise_prev=0.2)
+    s.device_state = device_state
+    with pytest.raises(RuntimeError, match="RoPE positions"):
+        s(m.core, x, mouse, btn, compile_on_decode=graphed)
+    torch.cuda.synchronize()
 
 
 def _dp_worker(rank, ws, port, q):
