@@ -202,8 +202,12 @@ int owlk_attn_bwd_dq(const void* q, long ldq, long sqb, const void* k, long ldk,
  * else the call runs write-through); bits 2-5 = chains of an XCD queue swept at a time (0 = all of
  * them interleaved; 1 gives each chain every workgroup of its XCD, so its sums and Q / dO tiles are
  * re-read fewer times); bit 1 = test mode: every contributor adds 1.0
- * instead of its dQ part and the last one keeps the fp32 sum in ws (dQ not written).  After the
- * call, ws int32 word 8 != 0 means a hand-off wait timed out (never expected). */
+ * instead of its dQ part and the last one keeps the fp32 sum in ws (dQ not written); bit 6 = test mode:
+ * chain 0's key block 1 times out on its hand-off waits.  A hand-off wait that times out (2 s; never
+ * expected) sets ws int32 word 8 to 1 and makes the tile's dQ NaN (every later part of the sum
+ * carries it, so the stored rows are NaN); after one timeout every later wait gives up at once.  In
+ * the XCD-local form a queue left undrained (no workgroup on its XCD) sets word 8 to 2 and its
+ * chains' dQ, dK and dV rows are written NaN.  No wrong gradient leaves the call looking valid. */
 long owlk_attn_bwd_fused_ws_bytes(long B, int H, long L, int head_dim);
 int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void* k, long ldk, long skb, const void* v,
                         long ldv, long svb, const void* dout, long ldo, long sob, const float* lse,

@@ -92,7 +92,7 @@ constexpr int MISC_OFF = FLAGL_OFF + 8 * 256;
 constexpr int JLO_OFF = MISC_OFF + 16;          // packed documents: per ring slot, its tile's first contributor
 constexpr int SMEM_BYTES = JLO_OFF + 2 * 256;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
-constexpr long HDR_BYTES = 256;                // [0, 8) dequeue counters, [8] error word, [9] keys per item
+constexpr long HDR_BYTES = 256;  // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
 // dQ^T products: 0 = 32x32x16 MFMAs on waves 0-3 (one 32 d x 32 q tile each); 1 = 16x16x32 MFMAs
 // on all 8 waves (one 16 d x 32 q quarter each: 50 % more LDS bytes, no idle waves)
@@ -125,6 +125,7 @@ struct FusedP {
   long fstride;
   int* jlo;                  // [B][jlo_stride]: each query tile's first contributing key block
   int jlo_stride;
+  int fail_chain;            // test mode (variant bit 6): chain 0's block-1 hand-off waits time out; else -1
 };
 
 DEV unsigned xcc_id() {
@@ -298,6 +299,10 @@ __global__ void fused_jlo_k(FusedP p, int B) {
   p.jlo[(long)b * p.jlo_stride + i] = v;
 }
 
+// test mode (variant bit 6): chain 0's block 1 waits for a flag value no block stores, so its hand-off
+// waits time out (after the spin bound) and take the error path
+DEV bool fail_at(const FusedP& p, int chain, int j) { return chain == p.fail_chain && j == 1; }
+
 // bounded poll of a flag word (every lane loads the same word: one request), sc1 loads
 DEV bool wait_flag(const int* f, int want, int* err) {
   if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= want)
@@ -370,10 +375,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   // generation of concurrent blocks re-sweeps the chain)
   auto item_of = [&](int x, int n, int& chain, int& jj) {
     const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
-    if (n >= cx * p.nkb) return false;
-    const int gfull = p.group * p.nkb, gi = n / gfull, m = n - gi * gfull;
-    const int gsz = cx - gi * p.group < p.group ? cx - gi * p.group : p.group;
-    chain = x + 8 * (gi * p.group + m % gsz);
+    if (n < 0 || (long)n >= (long)cx * p.nkb) return false;  // the host keeps cx * nkb < 2^31
+    const int grp = p.group < cx ? p.group : cx;               // group 1 << 20 = "all": no overflow
+    const int gfull = grp * p.nkb, gi = n / gfull, m = n - gi * gfull;
+    const int gsz = cx - gi * grp < grp ? cx - gi * grp : grp;
+    chain = x + 8 * (gi * grp + m % gsz);
     jj = m / gsz;
     return true;
   };
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const int x = (int)((xcc + d) & 7);
       const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
       if (cx == 0) continue;
-      if (__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cx * p.nkb) continue;
+      if ((long)__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (long)cx * p.nkb) continue;
       item_of(x, __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), chain, jj);
     }
   };
@@ -666,8 +672,14 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (!ready) {
-          wait_flag(flg + i * FLAG_STRIDE, j, p.hdr + 8);
-          load_acc(i);
+          if (wait_flag(flg + i * FLAG_STRIDE, fail_at(p, chain, j) ? 1 << 30 : j, p.hdr + 8)) {
+            load_acc(i);
+          } else {
+            // the predecessor's sum never arrived (the error word is set): this tile's dQ is void,
+            // and NaN carries that into every later part of it and into the stored dQ rows
+#pragma unroll
+            for (int e = 0; e < NACC; ++e) *(f32x4*)(accl + e * 1024 + lane * 16) = f32x4{NAN, NAN, NAN, NAN};
+          }
         }
         vm_wait<0>();  // the sum's loads are this wave's only vector-memory ops in flight here
 #pragma unroll
@@ -769,11 +781,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           issue_a(qbc);
           f32x4 st[2][2], dp[2][2];  // [16-row query tile][key tile]
           lgkm4<8>(lr[0], dr[0], lr[1], dr[1]);
-#pragma unroll
-          for (int qs = 0; qs < 2; ++qs) {
-            st[qs][0] = st[qs][1] = lr[qs];
-            dp[qs][0] = dp[qs][1] = dr[qs];
-          }
+          // the lse2 / delta rows are the first MFMA's C operand (no accumulator-init copies)
           static_for<2>([&](auto ksc) {
             constexpr int ks = decltype(ksc)::value;
             static_for<2>([&](auto qsc) {
@@ -781,8 +789,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
               lgkm2<6 - 4 * ks - 2 * qs>(aq[ks][qs], ad[ks][qs]);
 #pragma unroll
               for (int t2 = 0; t2 < 2; ++t2) {
-                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks][qs], kf[t2][ks], st[qs][t2], 0, 0, 0);
-                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[ks][qs], vf[t2][ks], dp[qs][t2], 0, 0, 0);
+                st[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks][qs], kf[t2][ks], ks ? st[qs][t2] : lr[qs], 0, 0, 0);
+                dp[qs][t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[ks][qs], vf[t2][ks], ks ? dp[qs][t2] : dr[qs], 0, 0, 0);
               }
             });
           });
@@ -848,7 +856,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         if constexpr (qb == 0) {
           if (poll) {  // the flag polled at the top has had half a tile to arrive
             vm_wait<0>();  // the dQ stores, the ring's DMA and the flag poll, in issue order
-            ready = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= j;  // 64 copies of one word
+            ready = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= (fail_at(p, chain, j) ? 1 << 30 : j);
             if (ready) {
               load_acc(t);
               loads_out = true;
@@ -922,6 +930,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
           *(bf16x4*)(stg + 4096 + off) = b4;
         }
       }
+      wave_lds_handoff();  // the rows were staged by other lanes of this wave
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
         const int r = 8 * it + (lane >> 3), x = lane & 7, k = kw0 + r;
@@ -959,6 +968,29 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       prof[4] += cb - ca;
       prof[5] += cc - cb;
       prof[6] += ce - cd;
+    }
+  }
+}
+
+// XCD-local form: every per-XCD queue must have been drained by workgroups running on that XCD.  A
+// queue no workgroup reached (an XCD left without workgroups, e.g. by a CU-masked stream) would leave
+// its chains' dK / dV / dQ unwritten with no sign.  One small launch after the sweep finds such a
+// queue, sets the error word (2) and writes NaN over every row of its chains' dQ, dK and dV.
+__global__ __launch_bounds__(256) void fused_drain_check_k(FusedP p) {
+  const int x = blockIdx.y;
+  const int cx = p.nchain > x ? (p.nchain - x + 7) / 8 : 0;
+  if ((long)__hip_atomic_load(p.hdr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (long)cx * p.nkb) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(p.hdr + 8, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bf16x8 nan8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) nan8[e] = (bf16)NAN;
+  for (int ch = x; ch < p.nchain; ch += 8) {
+    const int b = ch / p.H, head = ch % p.H;
+    for (long r = (long)blockIdx.x * 32 + (threadIdx.x >> 3); r < p.L; r += (long)gridDim.x * 32) {
+      const int col = head * 64 + 8 * (threadIdx.x & 7);
+      *(bf16x8*)(p.dq + b * p.sdqb + r * p.lddq + col) = nan8;
+      *(bf16x8*)(p.dk + b * p.sdkb + r * p.lddk + col) = nan8;
+      *(bf16x8*)(p.dv + b * p.sdvb + r * p.lddv + col) = nan8;
     }
   }
 }
@@ -1018,6 +1050,7 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   OWLK_REQUIRE(L < (1L << 31) / (tpf > 1 ? tpf : 1) || tpf == 1, "attn_bwd_fused: sequence too long");
   OWLK_REQUIRE(fused_tiles(L) * (long)ACC_TILE_BYTES < (1L << 31), "attn_bwd_fused: sequence too long");
   OWLK_REQUIRE(B * H < (1L << 24), "attn_bwd_fused: too many heads");
+  OWLK_REQUIRE((B * H / 8 + 1) * ((L + FKB - 1) / FKB) < (1L << 31), "attn_bwd_fused: too many work items per queue");
   const long need = owlk_attn_bwd_fused_ws_bytes(B, H, L, head_dim);
   OWLK_REQUIRE(ws && ws_bytes >= need && (uintptr_t)ws % 256 == 0, "attn_bwd_fused: workspace (%ld bytes, 256-B aligned) needed",
                need);
@@ -1052,6 +1085,7 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   p.fstride = fstride;
   p.jlo_stride = p.ntiles + 64;
   p.jlo = (int*)(p.acc + (long)p.nchain * p.ntiles * ACC_TILE_BYTES);
+  p.fail_chain = (variant & 64) ? 0 : -1;  // test mode: chain 0's block-1 hand-off waits time out
   hipStream_t s = (hipStream_t)stream;
   // counters, error word and flags are zero on entry (one memset node, 16-B multiple from the start)
   if (hipMemsetAsync(ws, 0, (size_t)(HDR_BYTES + (long)p.nchain * p.ntiles * FLAG_STRIDE * 4), s) != hipSuccess)
@@ -1069,13 +1103,19 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
       hipLaunchKernelGGL((attn_bwd_fused_k<true, false, true>), grid, dim3(512), 0, s, p);
     else
       hipLaunchKernelGGL((attn_bwd_fused_k<false, false, true>), grid, dim3(512), 0, s, p);
-    return owlk::check_launch("attn_bwd_fused");
+  } else {
+    switch (variant & 3) {
+      case 0: hipLaunchKernelGGL((attn_bwd_fused_k<false, false>), grid, dim3(512), 0, s, p); break;
+      case 1: hipLaunchKernelGGL((attn_bwd_fused_k<true, false>), grid, dim3(512), 0, s, p); break;
+      case 2: hipLaunchKernelGGL((attn_bwd_fused_k<false, true>), grid, dim3(512), 0, s, p); break;
+      default: hipLaunchKernelGGL((attn_bwd_fused_k<true, true>), grid, dim3(512), 0, s, p); break;
+    }
   }
-  switch (variant & 3) {
-    case 0: hipLaunchKernelGGL((attn_bwd_fused_k<false, false>), grid, dim3(512), 0, s, p); break;
-    case 1: hipLaunchKernelGGL((attn_bwd_fused_k<true, false>), grid, dim3(512), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((attn_bwd_fused_k<false, true>), grid, dim3(512), 0, s, p); break;
-    default: hipLaunchKernelGGL((attn_bwd_fused_k<true, true>), grid, dim3(512), 0, s, p); break;
+  if (int e = owlk::check_launch("attn_bwd_fused")) return e;
+  // the XCD-local form relies on workgroups reaching all 8 XCDs: check every queue was drained
+  if (variant & 1) {
+    hipLaunchKernelGGL(fused_drain_check_k, dim3(64, 8), dim3(256), 0, s, p);
+    return owlk::check_launch("attn_bwd_fused drain check");
   }
-  return owlk::check_launch("attn_bwd_fused");
+  return 0;
 }

@@ -771,6 +771,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
     }
   }
   if constexpr (STAGE) {
+    wave_lds_handoff();  // the rows were staged by other lanes of this wave
 #pragma unroll
     for (int it = 0; it < NQ * 2; ++it) {
       const int r = 8 * it + (lane >> 3), x = lane & 7;

@@ -21,6 +21,14 @@ DEV float rb(float x) {
   return __uint_as_float(u & 0xFFFF0000u);
 }
 DEV float bf2f(bf16 x) { return (float)x; }
+// lanes of one wave handing values to each other through LDS (a staging image written by some lanes,
+// read back by others): the compiler's memory model is per thread, so without this it may reorder a
+// lane's reads above its own writes when it proves their addresses differ.  Emits no instruction.
+DEV void wave_lds_handoff() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // sigmoid with v_rcp_f32 (1 ulp) instead of the IEEE division sequence (~10 VALU per element,
 // a tenth of a K = 1536 GEMM tile in the SiLU / dSiLU epilogues)

@@ -451,7 +451,10 @@ def fused_bwd_variant(D, mask):
     # one at a time (default) gives each chain the XCD's 32 workgroups: -2 % time and -54 % HBM
     # traffic against all three of dit_v4's at once (profiles/r4j_ab.log)
     group = int(os.environ.get("OWLK_BWD_FUSED_GROUP", "1"))
-    return (1 if env == "2" else 0) | (group & 15) << 2
+    # OWLK_BWD_FUSED_FAIL_TEST = 1 (tests only, variant bit 6): chain 0's block-1 hand-off waits time
+    # out, so the error path -- the error word and NaN dQ rows -- is exercised through this entry
+    fail = 64 if os.environ.get("OWLK_BWD_FUSED_FAIL_TEST") == "1" else 0
+    return (1 if env == "2" else 0) | (group & 15) << 2 | fail
 
 
 def attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, variant=0, ws=None):

@@ -126,6 +126,37 @@ def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
         assert rel(g, s) < 5e-3, name
 
 
+@pytest.mark.parametrize("variant_env", ["1", "2"])  # write-through, XCD-local
+def test_attention_bwd_fused_timeout_poisons_dq(variant_env, monkeypatch):
+    """A hand-off wait that times out cannot pass unnoticed: forced in test mode (variant bit 6: chain
+    0's key block 1 waits for a flag no block stores), kernels.attn_bwd -- the production entry --
+    returns NaN dQ rows (the tiles that block sweeps, and every tile whose wait gave up after it),
+    sets the error word, and leaves dK / dV (formed without the hand-off) finite (the model-level
+    consequence: tests/test_model_gpu.py::test_fused_handoff_timeout_reaches_the_loss).  Two 2-s spins
+    at most."""
+    k = K()
+    B, H, nf, tpf, D = 1, 2, 16, 64, 64
+    L = nf * tpf
+    q, kk, v, do = _inputs(B, H, L, D, 300)
+    mask = k.FrameMask(tpf, None, True)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+    monkeypatch.setenv("OWLK_BWD_FUSED", variant_env)
+    monkeypatch.setenv("OWLK_BWD_FUSED_FAIL_TEST", "1")
+    dq, dk, dv = (torch.zeros_like(q) for _ in range(3))
+    k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, dq, dk, dv)
+    torch.cuda.synchronize()
+    dq0 = dq.view(B, L, H, D)[:, :, 0]  # chain 0 = head 0
+    # block 1 (keys 256..511) sweeps query tiles 4.. (causal): their dQ is void
+    assert torch.isnan(dq0[:, 256:].float()).any(), "timed-out hand-off left no NaN in dQ"
+    assert torch.isfinite(dk.float()).all() and torch.isfinite(dv.float()).all()
+    # the raw entry reports it in the error word
+    delta = _delta(o, do, H, D)
+    ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, dq, dk, dv, D ** -0.5,
+                          k.fused_bwd_variant(D, mask))
+    torch.cuda.synchronize()
+    assert _hdr(ws)[8].item() == 1
+
+
 @pytest.mark.parametrize("case", [(2, 8, 48, 64, True, None), (1, 2, 40, 64, False, None), (1, 1, 300, 1, True, None),
                                   (1, 2, 48, 64, True, 16)])
 def test_attention_bwd_fused_deterministic(case):

@@ -397,7 +397,7 @@ def test_decode_positions_are_bounded(D):
     with pytest.raises(RuntimeError, match="rope table"):
         k.qk_rope_fwd(qkv, H, D, cos, sin, rows - L + 1, L)
     with pytest.raises(RuntimeError, match="rope table"):
-        k.qk_rope_fwd(qkv, H, D, cos, sin, 0, 0)  # T = B L rows from row 0: past the table
+        k.qk_rope_fwd(rnd(4 * L, 3 * H * D, seed=93), H, D, cos, sin, 0, 0)  # 256 rows from row 0, no wrap
     with pytest.raises(RuntimeError, match="rope table"):
         k.qk_rope_bwd(qkv[:, :2 * H * D].contiguous(), qkv, torch.ones(B * L, 2 * H, device=DEV), H, D, cos, sin,
                       torch.empty_like(qkv), rows - L + 1, L)

@@ -574,6 +574,27 @@ def test_device_state_decode_matches_host_state(d_model):
     assert torch.isfinite(outs[1]).all()
 
 
+def test_fused_handoff_timeout_reaches_the_loss(monkeypatch):
+    """A timed-out dQ hand-off of the single-pass backward (forced: OWLK_BWD_FUSED_FAIL_TEST, variant
+    bit 6) is not a silent wrong gradient: the qkv weight gradients come out non-finite, and after one
+    Muon / AdamW step (rft_trainer.py:186-199's consumer of the gradients) the next loss is NaN."""
+    from owl_wms.muon import init_muon
+    monkeypatch.setenv("OWLK_BWD_FUSED_FAIL_TEST", "1")
+    m, d = _run("bf16")
+    assert torch.isfinite(d["diffusion_loss"]).item()  # the forward is untouched
+    bad = [k for k, p in m.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
+    assert any("qkv" in k for k in bad), bad
+    opt = init_muon(m, lr=1e-3, momentum=0.95, adamw_lr=1e-4, adamw_wd=1e-4, adamw_eps=1e-15,
+                    adamw_betas=[0.9, 0.95], adamw_keys=["core.proj_in", "core.proj_out.proj", "core.t_embed",
+                                                         "core.control_embed", "gate", "adaln"])
+    opt.step()
+    monkeypatch.delenv("OWLK_BWD_FUSED_FAIL_TEST")
+    m.zero_grad(set_to_none=True)
+    d2 = m(GR["gamerft.bf16.in.x"].cuda(), GR["gamerft.bf16.in.mouse"].cuda(), GR["gamerft.bf16.in.btn"].cuda(),
+           GR["gamerft.bf16.in.doc_id"].cuda(), return_dict=True)
+    assert torch.isnan(d2["diffusion_loss"]).item()
+
+
 @pytest.mark.parametrize("device_state,graphed", [(False, False), (True, False), (True, True)])
 def test_decode_past_rope_table_raises(device_state, graphed):
     """Decoding past config.n_frames frames: the reference's rope slices cos[offset:offset + n] short
