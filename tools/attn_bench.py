@@ -125,7 +125,8 @@ def main():
                 print(f"  fused hand-offs (last call): {hw[10].item()} of {hw[11].item()} found the flag down at "
                       f"mid-step ({hw[10].item() / hw[11].item():.3f})", flush=True)
             for var in fvars:
-                nm = ("xcd-local" if var & 1 else "write-through") + (f" group {var >> 2}" if var >> 2 else "")
+                nm = ("xcd-local" if var & 1 else "write-through") + (f" group {(var >> 2) & 15}" if (var >> 2) & 15 else "") + \
+                    (" 1 wave/SIMD" if var & 128 else "")
                 t = min(t_fu[var])
                 print(f"  fused {t:8.3f} ms  {8 * D * pairs / t / 1e9:7.1f} TF/s alg (8 D pairs; 10 D executed: "
                       f"{10 * D * pairs / t / 1e9:.1f}) [{nm}: {t_fu[var]}] timeout word {err}", flush=True)
