@@ -410,7 +410,7 @@ def main():
                "data": f"synthetic (random latents of the {cfg_name} shape, random-init weights)",
                "config": {"workload": f"{args.config} training step: global batch {args.global_batch} x "
                                       f"{mc.n_frames} frames x 8x8 latents ({tokens} tokens/sample), fwd+bwd + "
-                                      f"RCCL grad all-reduce + Muon/AdamW step + EMA",
+                                      f"{'RCCL grad all-reduce + ' if world > 1 else ''}Muon/AdamW step + EMA",
                           "model": f"{cfg_name} ({mc.n_layers} L, d{mc.d_model}, {mc.n_heads} H, "
                                    f"{n_params / 1e6:.1f}M params)", "global_batch": args.global_batch,
                           "seq_len": tokens, "parallelism": f"dp{world}",

@@ -75,6 +75,20 @@
 #ifndef OWLK_FUSED_DQ_PF
 #define OWLK_FUSED_DQ_PF 3
 #endif
+#ifndef OWLK_FUSED_DMA47  // 1: the ring's LDS-DMA is issued by waves 4-7 only (no dQ work), 0: by all 8
+#define OWLK_FUSED_DMA47 1
+#endif
+// 1: wave w + 4 (no dQ work) polls the hand-off flag of dQ wave w and loads the predecessor's sum into
+// w's landing zone; the per-step flag store and the item claim are wave 4's too
+#ifndef OWLK_FUSED_HELP
+#define OWLK_FUSED_HELP 0
+#endif
+// 1 (with OWLK_FUSED_DMA47, HELP 0): the dQ waves poll the flag before their dQ products, so the
+// mid-step check waits for the poll only, not for the dQ stores issued after it
+#ifndef OWLK_FUSED_POLL_EARLY
+#define OWLK_FUSED_POLL_EARLY 0
+#endif
+static_assert(!OWLK_FUSED_POLL_EARLY || (OWLK_FUSED_DMA47 && !OWLK_FUSED_HELP), "POLL_EARLY: DMA47 and HELP 0");
 
 namespace {
 
@@ -90,7 +104,8 @@ constexpr int ACC_OFF = DS_OFF + 2 * DS_BYTES;  // per wave 2 KiB: its part of a
 constexpr int FLAGL_OFF = ACC_OFF + 8 * 2048;    // per wave 256 B: a polled flag word (64 copies)
 constexpr int MISC_OFF = FLAGL_OFF + 8 * 256;
 constexpr int JLO_OFF = MISC_OFF + 16;          // packed documents: per ring slot, its tile's first contributor
-constexpr int SMEM_BYTES = JLO_OFF + 2 * 256;
+constexpr int SYNC_OFF = JLO_OFF + 2 * 256;     // OWLK_FUSED_HELP: per dQ wave {landing zone free at step, sum loaded}
+constexpr int SMEM_BYTES = SYNC_OFF + 64;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
 constexpr long HDR_BYTES = 256;  // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
@@ -361,8 +376,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const int dch = (lane & 7) ^ swz_dual(drow);
   // (formed from an opaque lane id at each use: kept live across the sweep they were spilled, and
   // each reload's vmcnt(0) drained the dQ stores before the ring's DMA)
-  auto row_off = [&](int ld) {
-    const int ln = (int)opaque<1>((unsigned)lane), r = 8 * w + (ln >> 3);
+  // OWLK_FUSED_DMA47: waves 4-7 move rows 16 (w - 4) + 8 h + (lane >> 3) instead (h = 0, 1)
+  auto row_off = [&](int ld, int h = 0) {
+    const int ln = (int)opaque<1>((unsigned)lane);
+    const int r = OWLK_FUSED_DMA47 ? 16 * (w - 4) + 8 * h + (ln >> 3) : 8 * w + (ln >> 3);
     return (unsigned)((r * ld + (((ln & 7) ^ swz_dual(r)) * 8)) * 2);
   };
 
@@ -395,12 +412,19 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       item_of(x, __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), chain, jj);
     }
   };
-  if (OWLK_FUSED_DEQ_PF && threadIdx.x == 0) claim(0, sh_item[0], sh_item[1]);
+  // the item claims and the per-step flag stores: one lane of a wave without dQ work (OWLK_FUSED_HELP)
+  const bool leader = threadIdx.x == (OWLK_FUSED_HELP ? 256u : 0u);
+  int* zone_free = (int*)(smem + SYNC_OFF);       // [dQ wave]: the global step whose top it read its zone at
+  int* zone_full = (int*)(smem + SYNC_OFF + 32);  // [dQ wave]: 1 = the helper loaded the polled sum
+  // (zone_free[4 + w], HELP 2: the step whose sum the helper of dQ wave w has landed)
+  unsigned gstep = 0;  // steps of this workgroup so far (never repeats across items)
+  bool helped = false;  // HELP 2: this helper wave's sum loads are in flight over the barrier
+  if (OWLK_FUSED_DEQ_PF && leader) claim(0, sh_item[0], sh_item[1]);
   for (;;) {
     const unsigned long long ca = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local);
     // OWLK_FUSED_DEQ_PF: claimed during the previous item's epilogue
-    if (!OWLK_FUSED_DEQ_PF && threadIdx.x == 0) {
+    if (!OWLK_FUSED_DEQ_PF && leader) {
       int chain, jj;
       claim(0, chain, jj);
       sh_item[0] = chain;
@@ -459,6 +483,30 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     auto issue = [&](int t) {
       char* buf = smem + (t & 1) * RING_SLOT;
       const int q0 = t * FQT;
+      if (OWLK_FUSED_DMA47) {
+        // the waves without dQ work issue the whole tile (the dQ waves are each step's critical path)
+        if (w < 4) return;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          char* dst = buf + (16 * (w - 4) + 8 * h) * 128;
+          if (q0 + FQT <= L) {
+            dma16(lds_addr(dst), Q + (long)q0 * p.ldq, row_off(p.ldq, h));
+            dma16(lds_addr(dst + TILE_BYTES), dO + (long)q0 * p.ldo, row_off(p.ldo, h));
+          } else {
+            const int r = 16 * (w - 4) + 8 * h + (lane >> 3), ch = (lane & 7) ^ swz_dual(r);
+            int gr = q0 + r;
+            gr = gr < L ? gr : L - 1;
+            dma16(lds_addr(dst), Q + (long)q0 * p.ldq, (unsigned)(((gr - q0) * p.ldq + ch * 8) * 2));
+            dma16(lds_addr(dst + TILE_BYTES), dO + (long)q0 * p.ldo, (unsigned)(((gr - q0) * p.ldo + ch * 8) * 2));
+          }
+        }
+        if (w < 6) {
+          const int src = q0 + lane < L ? lane : L - 1 - q0;
+          dma4(lds_addr(buf + 2 * TILE_BYTES + (w - 4) * FQT * 4), (w == 5 ? DLT : LSE) + q0, (unsigned)(src * 4));
+        }
+        if (RUNS && w == 6) dma4(lds_addr(smem + JLO_OFF + (t & 1) * 256), jlo_row + t, (unsigned)(lane * 4));
+        return;
+      }
       if (q0 + FQT <= L) {
         dma16(lds_addr(buf + 8 * w * 128), Q + (long)q0 * p.ldq, row_off(p.ldq));
         dma16(lds_addr(buf + TILE_BYTES + 8 * w * 128), dO + (long)q0 * p.ldo, row_off(p.ldo));
@@ -503,8 +551,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     // none of them sees, else PARTIAL
     const bool wave_live = kw0 < L;
     const int wfk0 = frame(p, kw0), wfk1 = frame(p, kw0 + 31 < L ? kw0 + 31 : L - 1);
-    const long seen_lo = (long)q_lo_frame(p, wfk0) * p.tpf,
-               seen_hi = RUNS ? q_hi_end_runs(p, qh, wfk1) : q_hi_end(p, wfk1);  // any key
+    const int seen_lo = __builtin_amdgcn_readfirstlane((int)((long)q_lo_frame(p, wfk0) * p.tpf)),
+              seen_hi = __builtin_amdgcn_readfirstlane((int)(RUNS ? q_hi_end_runs(p, qh, wfk1) : q_hi_end(p, wfk1)));
     int full_lo = (int)(((long)q_lo_frame(p, wfk1) * p.tpf + FQT - 1) / FQT);
     int full_hi = (int)((RUNS ? q_hi_end_runs(p, qh, wfk0) : q_hi_end(p, wfk0)) / FQT);  // exclusive: whole tiles only
     // packed documents: this lane's keys' row ends, for the PARTIAL tiles' masks
@@ -588,6 +636,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
       for (int e = 0; e < NACC; ++e) dma16_sc1(lds_addr(accl + e * 1024), accp + (long)i * ACC_TILE_BYTES + e * 1024, acc_lane);
     };
+    // OWLK_FUSED_HELP: helper wave w (4-7) loads dQ wave w - 4's part of tile i's sum into that wave's zone
+    auto load_acc_for = [&](int i) {
+      const int ww = w - 4;
+      char* zone = smem + ACC_OFF + ww * NACC * 1024;
+#pragma unroll
+      for (int e = 0; e < NACC; ++e)
+        dma16_sc1(lds_addr(zone + e * 1024), accp + (long)i * ACC_TILE_BYTES + e * 1024,
+                  (unsigned)(ww * NACC * 1024 + lane * 16));
+    };
 
     // dQ^T[32 d x 32 q] of tile i += K^T[32 d x 16 keys] dS^T[16 keys x 32 q] over the item's keys,
     // from the K image and the tile's dS image (written in the tile's own step); both fragments in
@@ -667,6 +724,14 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
       for (int e = 0; e < NACC; ++e) a[e] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (j > jlo_at(i) && !(OWLK_FUSED_EXP & 1)) {
+        if (OWLK_FUSED_HELP) {
+          ready = __builtin_amdgcn_readfirstlane(zone_full[w]) != 0;
+          // HELP 2: the helper's loads were left in flight over the barrier; it stamps the step
+          // they landed for at its next step's top
+          if (OWLK_FUSED_HELP == 2 && ready)
+            while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_free[4 + w]) != (int)gstep - 1)
+              __builtin_amdgcn_s_sleep(1);
+        }
         if (OWLK_FUSED_STATS && lane == 0) {
           __hip_atomic_fetch_add(p.hdr + 11, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -685,6 +750,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
         for (int e = 0; e < NACC; ++e) a[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
       }
+      if (OWLK_FUSED_HELP) {
+        // the zone has been read (the loads above returned: they are used below); the helper may refill it
+        wave_lds_handoff();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) zone_free[w] = (int)gstep;
+      }
       if constexpr (DQ16) {
         qa[0] = a[0];
         qa[1] = a[1];
@@ -700,12 +771,21 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const int q0 = t * FQT;
       const unsigned long long c0 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dq_on = !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi && dq_wave;
+      ++gstep;
+      if (OWLK_FUSED_HELP == 2 && !dq_wave && helped) {
+        vm_wait<0>();  // the sum this wave loaded last step for wave w - 4 has landed
+        if (lane == 0) zone_free[w] = (int)gstep - 1;
+        helped = false;
+      }
       // the predecessor's sum of tile t + 1 (waits for this wave's vector memory: before any DMA)
       if (dq_on) dq_begin(t + 1);
+      else if (OWLK_FUSED_HELP && dq_wave && lane == 0) zone_free[w] = (int)gstep;
+      const bool poll = j > jlo_at(t) && (OWLK_FUSED_HELP ? !dq_wave : dq_wave) && !(OWLK_FUSED_EXP & 1);
+      if (OWLK_FUSED_POLL_EARLY && poll) dma4_sc1(lds_addr(smem + FLAGL_OFF + w * 256), flg + t * FLAG_STRIDE, 0u);
 
       int kind = TILE_FULL;
       if (t < full_lo || t >= full_hi) {
-        const long r1 = q0 + FQT < L ? q0 + FQT : L;
+        const int r1 = q0 + FQT < L ? q0 + FQT : L;
         kind = !wave_live || r1 <= seen_lo || q0 >= seen_hi ? TILE_EMPTY : TILE_PARTIAL;
       }
       kind = __builtin_amdgcn_readfirstlane(kind);
@@ -746,8 +826,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const unsigned long long c1 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dma = t - 1 >= t_lo;
       if (dma) issue(t - 1);
-      const bool poll = j > jlo_at(t) && dq_wave && !(OWLK_FUSED_EXP & 1);
-      if (poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
+      if (!OWLK_FUSED_POLL_EARLY && poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
 
       const unsigned dsw = lds_addr(smem + DS_OFF + (t & 1) * DS_BYTES) + dsl;
       auto ds_put = [&](int t2, int qb, int e, bf16x4 v) {
@@ -855,11 +934,31 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         }
         if constexpr (qb == 0) {
           if (poll) {  // the flag polled at the top has had half a tile to arrive
-            vm_wait<0>();  // the dQ stores, the ring's DMA and the flag poll, in issue order
-            ready = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= (fail_at(p, chain, j) ? 1 << 30 : j);
-            if (ready) {
-              load_acc(t);
-              loads_out = true;
+            // the dQ stores, the ring's DMA and the flag poll, in issue order (POLL_EARLY: the poll,
+            // then the NACC dQ stores, which may stay in flight)
+            if (OWLK_FUSED_POLL_EARLY && dq_on)
+              vm_wait<NACC>();
+            else
+              vm_wait<0>();
+            const bool up = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= (fail_at(p, chain, j) ? 1 << 30 : j);
+            if (OWLK_FUSED_HELP) {
+              // wave w - 4 read its zone at this step's top (it says so in LDS); then refill it
+              if (up) {
+                while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_free[w - 4]) != (int)gstep)
+                  __builtin_amdgcn_s_sleep(1);
+                load_acc_for(t);
+                if (OWLK_FUSED_HELP == 2) {
+                  loads_out = true;
+                  helped = true;
+                }
+              }
+              if (lane == 0) zone_full[w - 4] = up ? 1 : 0;
+            } else {
+              ready = up;
+              if (ready) {
+                load_acc(t);
+                loads_out = true;
+              }
             }
           }
         }
@@ -880,17 +979,23 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         prof[2] += c3 - c2;
         prof[3] += c4 - c3;
       }
-      if (t + 1 <= t_hi && threadIdx.x == 0)
+      if (t + 1 <= t_hi && leader)
         __hip_atomic_store(flg + (t + 1) * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
     const unsigned long long cd = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const bool dq_epi = !(OWLK_FUSED_EXP & 2) && dq_wave;
+    ++gstep;
+    if (OWLK_FUSED_HELP == 2 && !dq_wave && helped) {
+      vm_wait<0>();
+      if (lane == 0) zone_free[w] = (int)gstep - 1;
+      helped = false;
+    }
     if (dq_epi) dq_begin(t_lo);
     // the next item's claim on this XCD's queue: its return is waited for with the dQ stores
     int npf = 0;
-    if (OWLK_FUSED_DEQ_PF && threadIdx.x == 0)
+    if (OWLK_FUSED_DEQ_PF && leader)
       npf = __hip_atomic_fetch_add(p.hdr + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dq_epi) {
       dq_mfma(t_lo);
@@ -898,7 +1003,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     }
     vm_wait<0>();
     __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
-    if (threadIdx.x == 0) {
+    if (leader) {
       __hip_atomic_store(flg + t_lo * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (OWLK_FUSED_DEQ_PF) {
         int nc = -1, nj = 0;
