@@ -89,6 +89,13 @@
 #define OWLK_FUSED_POLL_EARLY 0
 #endif
 static_assert(!OWLK_FUSED_POLL_EARLY || (OWLK_FUSED_DMA47 && !OWLK_FUSED_HELP), "POLL_EARLY: DMA47 and HELP 0");
+// 1: a tile's dQ^T products are split over the item's two key halves: dQ wave w sums keys 0-127 onto
+// the predecessor's sum, wave w + 4 keys 128-255 from zero and hands its part over through w's landing
+// zone (an LDS word each way); the dQ waves' step gets 8 of the 16 32x32x16 products off its path
+#ifndef OWLK_FUSED_DQSPLIT
+#define OWLK_FUSED_DQSPLIT 0
+#endif
+static_assert(!OWLK_FUSED_DQSPLIT || (OWLK_FUSED_DMA47 && !OWLK_FUSED_HELP), "DQSPLIT: DMA47 and HELP 0");
 
 namespace {
 
@@ -418,6 +425,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   int* zone_full = (int*)(smem + SYNC_OFF + 32);  // [dQ wave]: 1 = the helper loaded the polled sum
   // (zone_free[4 + w], HELP 2: the step whose sum the helper of dQ wave w has landed)
   unsigned gstep = 0;  // steps of this workgroup so far (never repeats across items)
+  if (threadIdx.x < 16) ((int*)(smem + SYNC_OFF))[threadIdx.x] = -1;  // no stale step stamps (first barrier below)
   bool helped = false;  // HELP 2: this helper wave's sum loads are in flight over the barrier
   if (OWLK_FUSED_DEQ_PF && leader) claim(0, sh_item[0], sh_item[1]);
   for (;;) {
@@ -650,8 +658,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     // from the K image and the tile's dS image (written in the tile's own step); both fragments in
     // frag_tr's permuted row order (the same for A and B), software-pipelined OWLK_FUSED_DQ_PF
     // k-steps deep
-    auto dq_mfma = [&](int i) {
+    // h: key half (OWLK_FUSED_DQSPLIT: 0 = keys 0-127 on the dQ wave, 1 = keys 128-255 on its helper;
+    // -1 = all 256 keys)
+    auto dq_mfma = [&](int i, int h = -1) {
       if constexpr (counting) {
+        if (h == 1) return;  // the dQ wave's half adds the block's 1.0
 #pragma unroll
         for (int e = 0; e < 16; ++e) qacc[e] += 1.f;
 #pragma unroll
@@ -688,8 +699,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         });
         return;
       }
-      constexpr int NK = FKB / 16, PF = OWLK_FUSED_DQ_PF;
-      const unsigned kb0 = lds_addr(kimg), sb0 = lds_addr(smem + DS_OFF + (i & 1) * DS_BYTES);
+      constexpr int NK = FKB / 16 / (OWLK_FUSED_DQSPLIT ? 2 : 1), PF = OWLK_FUSED_DQ_PF;
+      const unsigned hoff = OWLK_FUSED_DQSPLIT && h == 1 ? (unsigned)(NK * 2048) : 0u;  // 16-key k steps of 2 KiB
+      const unsigned kb0 = lds_addr(kimg) + hoff, sb0 = lds_addr(smem + DS_OFF + (i & 1) * DS_BYTES) + hoff;
       const unsigned ka = kb0 + ok32a, kb = kb0 + ok32b, sa = sb0 + os32a, sb = sb0 + os32b;
       s16x4 r[PF + 1][4];
       auto rd = [&](auto kc) {
@@ -708,6 +720,30 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         qacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(join_tr(r[sl][0], r[sl][1]), join_tr(r[sl][2], r[sl][3]), qacc,
                                                        0, 0, 0);
       });
+    };
+
+    // OWLK_FUSED_DQSPLIT, dQ wave: add the helper's half of tile i's products (after its own half)
+    auto dq_join = [&]() {
+      while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_full[w]) != (int)gstep) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int e = 0; e < NACC; ++e) {
+        const f32x4 v = *(const f32x4*)(accl + e * 1024 + lane * 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qacc[4 * e + r] += v[r];
+      }
+    };
+    // ... helper wave w (4-7): its half from zero into dQ wave w - 4's zone, once that wave has read it
+    auto dq_help = [&](int i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) qacc[e] = 0.f;
+      while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_free[w - 4]) != (int)gstep) __builtin_amdgcn_s_sleep(1);
+      dq_mfma(i, 1);
+      char* zone = smem + ACC_OFF + (w - 4) * NACC * 1024;
+#pragma unroll
+      for (int e = 0; e < NACC; ++e)
+        *(f32x4*)(zone + e * 1024 + lane * 16) = f32x4{qacc[4 * e], qacc[4 * e + 1], qacc[4 * e + 2], qacc[4 * e + 3]};
+      wave_lds_handoff();
+      if (lane == 0) *(volatile int*)&zone_full[w - 4] = (int)gstep;  // after the part, in LDS order
     };
 
     issue(t_hi);
@@ -750,7 +786,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
         for (int e = 0; e < NACC; ++e) a[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
       }
-      if (OWLK_FUSED_HELP) {
+      if (OWLK_FUSED_HELP || OWLK_FUSED_DQSPLIT) {
         // the zone has been read (the loads above returned: they are used below); the helper may refill it
         wave_lds_handoff();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -819,13 +855,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       // dQ of tile t + 1 from its dS image (step t + 1), stored at once; this step's barrier drains
       // the stores, then the flag goes out
       if (dq_on) {
-        dq_mfma(t + 1);
+        dq_mfma(t + 1, OWLK_FUSED_DQSPLIT ? 0 : -1);
+        if (OWLK_FUSED_DQSPLIT) dq_join();
         store_dq(t + 1);
       }
       // in issue order: the dQ stores, the ring's LDS-DMA of tile t - 1, the flag poll
       const unsigned long long c1 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dma = t - 1 >= t_lo;
       if (dma) issue(t - 1);
+      if (OWLK_FUSED_DQSPLIT && !dq_wave && !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi) dq_help(t + 1);
       if (!OWLK_FUSED_POLL_EARLY && poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
 
       const unsigned dsw = lds_addr(smem + DS_OFF + (t & 1) * DS_BYTES) + dsl;
@@ -998,9 +1036,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
     if (OWLK_FUSED_DEQ_PF && leader)
       npf = __hip_atomic_fetch_add(p.hdr + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dq_epi) {
-      dq_mfma(t_lo);
+      dq_mfma(t_lo, OWLK_FUSED_DQSPLIT ? 0 : -1);
+      if (OWLK_FUSED_DQSPLIT) dq_join();
       store_dq(t_lo);
     }
+    if (OWLK_FUSED_DQSPLIT && !dq_wave && !(OWLK_FUSED_EXP & 2)) dq_help(t_lo);
     vm_wait<0>();
     __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
     if (leader) {
