@@ -78,24 +78,6 @@
 #ifndef OWLK_FUSED_DMA47  // 1: the ring's LDS-DMA is issued by waves 4-7 only (no dQ work), 0: by all 8
 #define OWLK_FUSED_DMA47 1
 #endif
-// 1: wave w + 4 (no dQ work) polls the hand-off flag of dQ wave w and loads the predecessor's sum into
-// w's landing zone; the per-step flag store and the item claim are wave 4's too
-#ifndef OWLK_FUSED_HELP
-#define OWLK_FUSED_HELP 0
-#endif
-// 1 (with OWLK_FUSED_DMA47, HELP 0): the dQ waves poll the flag before their dQ products, so the
-// mid-step check waits for the poll only, not for the dQ stores issued after it
-#ifndef OWLK_FUSED_POLL_EARLY
-#define OWLK_FUSED_POLL_EARLY 0
-#endif
-static_assert(!OWLK_FUSED_POLL_EARLY || (OWLK_FUSED_DMA47 && !OWLK_FUSED_HELP), "POLL_EARLY: DMA47 and HELP 0");
-// 1: a tile's dQ^T products are split over the item's two key halves: dQ wave w sums keys 0-127 onto
-// the predecessor's sum, wave w + 4 keys 128-255 from zero and hands its part over through w's landing
-// zone (an LDS word each way); the dQ waves' step gets 8 of the 16 32x32x16 products off its path
-#ifndef OWLK_FUSED_DQSPLIT
-#define OWLK_FUSED_DQSPLIT 0
-#endif
-static_assert(!OWLK_FUSED_DQSPLIT || (OWLK_FUSED_DMA47 && !OWLK_FUSED_HELP), "DQSPLIT: DMA47 and HELP 0");
 
 namespace {
 
@@ -111,8 +93,7 @@ constexpr int ACC_OFF = DS_OFF + 2 * DS_BYTES;  // per wave 2 KiB: its part of a
 constexpr int FLAGL_OFF = ACC_OFF + 8 * 2048;    // per wave 256 B: a polled flag word (64 copies)
 constexpr int MISC_OFF = FLAGL_OFF + 8 * 256;
 constexpr int JLO_OFF = MISC_OFF + 16;          // packed documents: per ring slot, its tile's first contributor
-constexpr int SYNC_OFF = JLO_OFF + 2 * 256;     // OWLK_FUSED_HELP: per dQ wave {landing zone free at step, sum loaded}
-constexpr int SMEM_BYTES = SYNC_OFF + 64;
+constexpr int SMEM_BYTES = JLO_OFF + 2 * 256;
 constexpr int FLAG_STRIDE = 16;                // ints: one 64-B line per query-tile flag
 constexpr long HDR_BYTES = 256;  // [0, 8) dequeue counters, [8] error word, [9] keys per item
 constexpr int ACC_TILE_BYTES = FQT * 64 * 4;   // fp32 accumulator of one query tile
@@ -419,20 +400,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       item_of(x, __hip_atomic_fetch_add(p.hdr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), chain, jj);
     }
   };
-  // the item claims and the per-step flag stores: one lane of a wave without dQ work (OWLK_FUSED_HELP)
-  const bool leader = threadIdx.x == (OWLK_FUSED_HELP ? 256u : 0u);
-  int* zone_free = (int*)(smem + SYNC_OFF);       // [dQ wave]: the global step whose top it read its zone at
-  int* zone_full = (int*)(smem + SYNC_OFF + 32);  // [dQ wave]: 1 = the helper loaded the polled sum
-  // (zone_free[4 + w], HELP 2: the step whose sum the helper of dQ wave w has landed)
-  unsigned gstep = 0;  // steps of this workgroup so far (never repeats across items)
-  if (threadIdx.x < 16) ((int*)(smem + SYNC_OFF))[threadIdx.x] = -1;  // no stale step stamps (first barrier below)
-  bool helped = false;  // HELP 2: this helper wave's sum loads are in flight over the barrier
-  if (OWLK_FUSED_DEQ_PF && leader) claim(0, sh_item[0], sh_item[1]);
+  if (OWLK_FUSED_DEQ_PF && threadIdx.x == 0) claim(0, sh_item[0], sh_item[1]);
   for (;;) {
     const unsigned long long ca = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     // ---- dequeue: the next item of this XCD's queue (others' when it is empty, unless local);
     // OWLK_FUSED_DEQ_PF: claimed during the previous item's epilogue
-    if (!OWLK_FUSED_DEQ_PF && leader) {
+    if (!OWLK_FUSED_DEQ_PF && threadIdx.x == 0) {
       int chain, jj;
       claim(0, chain, jj);
       sh_item[0] = chain;
@@ -644,25 +617,13 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
       for (int e = 0; e < NACC; ++e) dma16_sc1(lds_addr(accl + e * 1024), accp + (long)i * ACC_TILE_BYTES + e * 1024, acc_lane);
     };
-    // OWLK_FUSED_HELP: helper wave w (4-7) loads dQ wave w - 4's part of tile i's sum into that wave's zone
-    auto load_acc_for = [&](int i) {
-      const int ww = w - 4;
-      char* zone = smem + ACC_OFF + ww * NACC * 1024;
-#pragma unroll
-      for (int e = 0; e < NACC; ++e)
-        dma16_sc1(lds_addr(zone + e * 1024), accp + (long)i * ACC_TILE_BYTES + e * 1024,
-                  (unsigned)(ww * NACC * 1024 + lane * 16));
-    };
 
     // dQ^T[32 d x 32 q] of tile i += K^T[32 d x 16 keys] dS^T[16 keys x 32 q] over the item's keys,
     // from the K image and the tile's dS image (written in the tile's own step); both fragments in
     // frag_tr's permuted row order (the same for A and B), software-pipelined OWLK_FUSED_DQ_PF
     // k-steps deep
-    // h: key half (OWLK_FUSED_DQSPLIT: 0 = keys 0-127 on the dQ wave, 1 = keys 128-255 on its helper;
-    // -1 = all 256 keys)
-    auto dq_mfma = [&](int i, int h = -1) {
+    auto dq_mfma = [&](int i) {
       if constexpr (counting) {
-        if (h == 1) return;  // the dQ wave's half adds the block's 1.0
 #pragma unroll
         for (int e = 0; e < 16; ++e) qacc[e] += 1.f;
 #pragma unroll
@@ -699,9 +660,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         });
         return;
       }
-      constexpr int NK = FKB / 16 / (OWLK_FUSED_DQSPLIT ? 2 : 1), PF = OWLK_FUSED_DQ_PF;
-      const unsigned hoff = OWLK_FUSED_DQSPLIT && h == 1 ? (unsigned)(NK * 2048) : 0u;  // 16-key k steps of 2 KiB
-      const unsigned kb0 = lds_addr(kimg) + hoff, sb0 = lds_addr(smem + DS_OFF + (i & 1) * DS_BYTES) + hoff;
+      constexpr int NK = FKB / 16, PF = OWLK_FUSED_DQ_PF;
+      const unsigned kb0 = lds_addr(kimg), sb0 = lds_addr(smem + DS_OFF + (i & 1) * DS_BYTES);
       const unsigned ka = kb0 + ok32a, kb = kb0 + ok32b, sa = sb0 + os32a, sb = sb0 + os32b;
       s16x4 r[PF + 1][4];
       auto rd = [&](auto kc) {
@@ -722,30 +682,6 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       });
     };
 
-    // OWLK_FUSED_DQSPLIT, dQ wave: add the helper's half of tile i's products (after its own half)
-    auto dq_join = [&]() {
-      while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_full[w]) != (int)gstep) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int e = 0; e < NACC; ++e) {
-        const f32x4 v = *(const f32x4*)(accl + e * 1024 + lane * 16);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) qacc[4 * e + r] += v[r];
-      }
-    };
-    // ... helper wave w (4-7): its half from zero into dQ wave w - 4's zone, once that wave has read it
-    auto dq_help = [&](int i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) qacc[e] = 0.f;
-      while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_free[w - 4]) != (int)gstep) __builtin_amdgcn_s_sleep(1);
-      dq_mfma(i, 1);
-      char* zone = smem + ACC_OFF + (w - 4) * NACC * 1024;
-#pragma unroll
-      for (int e = 0; e < NACC; ++e)
-        *(f32x4*)(zone + e * 1024 + lane * 16) = f32x4{qacc[4 * e], qacc[4 * e + 1], qacc[4 * e + 2], qacc[4 * e + 3]};
-      wave_lds_handoff();
-      if (lane == 0) *(volatile int*)&zone_full[w - 4] = (int)gstep;  // after the part, in LDS order
-    };
-
     issue(t_hi);
     vm_wait<0>();
     __syncthreads();
@@ -760,14 +696,6 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
       for (int e = 0; e < NACC; ++e) a[e] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (j > jlo_at(i) && !(OWLK_FUSED_EXP & 1)) {
-        if (OWLK_FUSED_HELP) {
-          ready = __builtin_amdgcn_readfirstlane(zone_full[w]) != 0;
-          // HELP 2: the helper's loads were left in flight over the barrier; it stamps the step
-          // they landed for at its next step's top
-          if (OWLK_FUSED_HELP == 2 && ready)
-            while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_free[4 + w]) != (int)gstep - 1)
-              __builtin_amdgcn_s_sleep(1);
-        }
         if (OWLK_FUSED_STATS && lane == 0) {
           __hip_atomic_fetch_add(p.hdr + 11, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (!ready) __hip_atomic_fetch_add(p.hdr + 10, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -786,12 +714,6 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
 #pragma unroll
         for (int e = 0; e < NACC; ++e) a[e] = *(const f32x4*)(accl + e * 1024 + lane * 16);
       }
-      if (OWLK_FUSED_HELP || OWLK_FUSED_DQSPLIT) {
-        // the zone has been read (the loads above returned: they are used below); the helper may refill it
-        wave_lds_handoff();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) zone_free[w] = (int)gstep;
-      }
       if constexpr (DQ16) {
         qa[0] = a[0];
         qa[1] = a[1];
@@ -807,17 +729,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       const int q0 = t * FQT;
       const unsigned long long c0 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dq_on = !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi && dq_wave;
-      ++gstep;
-      if (OWLK_FUSED_HELP == 2 && !dq_wave && helped) {
-        vm_wait<0>();  // the sum this wave loaded last step for wave w - 4 has landed
-        if (lane == 0) zone_free[w] = (int)gstep - 1;
-        helped = false;
-      }
       // the predecessor's sum of tile t + 1 (waits for this wave's vector memory: before any DMA)
       if (dq_on) dq_begin(t + 1);
-      else if (OWLK_FUSED_HELP && dq_wave && lane == 0) zone_free[w] = (int)gstep;
-      const bool poll = j > jlo_at(t) && (OWLK_FUSED_HELP ? !dq_wave : dq_wave) && !(OWLK_FUSED_EXP & 1);
-      if (OWLK_FUSED_POLL_EARLY && poll) dma4_sc1(lds_addr(smem + FLAGL_OFF + w * 256), flg + t * FLAG_STRIDE, 0u);
+      const bool poll = j > jlo_at(t) && dq_wave && !(OWLK_FUSED_EXP & 1);
 
       int kind = TILE_FULL;
       if (t < full_lo || t >= full_hi) {
@@ -855,16 +769,14 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
       // dQ of tile t + 1 from its dS image (step t + 1), stored at once; this step's barrier drains
       // the stores, then the flag goes out
       if (dq_on) {
-        dq_mfma(t + 1, OWLK_FUSED_DQSPLIT ? 0 : -1);
-        if (OWLK_FUSED_DQSPLIT) dq_join();
+        dq_mfma(t + 1);
         store_dq(t + 1);
       }
       // in issue order: the dQ stores, the ring's LDS-DMA of tile t - 1, the flag poll
       const unsigned long long c1 = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
       const bool dma = t - 1 >= t_lo;
       if (dma) issue(t - 1);
-      if (OWLK_FUSED_DQSPLIT && !dq_wave && !(OWLK_FUSED_EXP & 2) && t + 1 <= t_hi) dq_help(t + 1);
-      if (!OWLK_FUSED_POLL_EARLY && poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
+      if (poll) dma4_sc1(lds_addr(flagl), flg + t * FLAG_STRIDE, 0u);
 
       const unsigned dsw = lds_addr(smem + DS_OFF + (t & 1) * DS_BYTES) + dsl;
       auto ds_put = [&](int t2, int qb, int e, bf16x4 v) {
@@ -972,31 +884,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         }
         if constexpr (qb == 0) {
           if (poll) {  // the flag polled at the top has had half a tile to arrive
-            // the dQ stores, the ring's DMA and the flag poll, in issue order (POLL_EARLY: the poll,
-            // then the NACC dQ stores, which may stay in flight)
-            if (OWLK_FUSED_POLL_EARLY && dq_on)
-              vm_wait<NACC>();
-            else
-              vm_wait<0>();
-            const bool up = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= (fail_at(p, chain, j) ? 1 << 30 : j);
-            if (OWLK_FUSED_HELP) {
-              // wave w - 4 read its zone at this step's top (it says so in LDS); then refill it
-              if (up) {
-                while (__builtin_amdgcn_readfirstlane(*(volatile int*)&zone_free[w - 4]) != (int)gstep)
-                  __builtin_amdgcn_s_sleep(1);
-                load_acc_for(t);
-                if (OWLK_FUSED_HELP == 2) {
-                  loads_out = true;
-                  helped = true;
-                }
-              }
-              if (lane == 0) zone_full[w - 4] = up ? 1 : 0;
-            } else {
-              ready = up;
-              if (ready) {
-                load_acc(t);
-                loads_out = true;
-              }
+            vm_wait<0>();  // the dQ stores and the flag poll, in issue order (the dQ waves issue no ring DMA)
+            ready = __builtin_amdgcn_readfirstlane(*(const int*)flagl) >= (fail_at(p, chain, j) ? 1 << 30 : j);
+            if (ready) {
+              load_acc(t);
+              loads_out = true;
             }
           }
         }
@@ -1017,33 +909,25 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
         prof[2] += c3 - c2;
         prof[3] += c4 - c3;
       }
-      if (t + 1 <= t_hi && leader)
+      if (t + 1 <= t_hi && threadIdx.x == 0)
         __hip_atomic_store(flg + (t + 1) * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // ---- epilogue: dQ of tile t_lo (its dS image is in LDS)
     const unsigned long long cd = OWLK_FUSED_PROF ? __builtin_amdgcn_s_memtime() : 0ull;
     const bool dq_epi = !(OWLK_FUSED_EXP & 2) && dq_wave;
-    ++gstep;
-    if (OWLK_FUSED_HELP == 2 && !dq_wave && helped) {
-      vm_wait<0>();
-      if (lane == 0) zone_free[w] = (int)gstep - 1;
-      helped = false;
-    }
     if (dq_epi) dq_begin(t_lo);
     // the next item's claim on this XCD's queue: its return is waited for with the dQ stores
     int npf = 0;
-    if (OWLK_FUSED_DEQ_PF && leader)
+    if (OWLK_FUSED_DEQ_PF && threadIdx.x == 0)
       npf = __hip_atomic_fetch_add(p.hdr + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dq_epi) {
-      dq_mfma(t_lo, OWLK_FUSED_DQSPLIT ? 0 : -1);
-      if (OWLK_FUSED_DQSPLIT) dq_join();
+      dq_mfma(t_lo);
       store_dq(t_lo);
     }
-    if (OWLK_FUSED_DQSPLIT && !dq_wave && !(OWLK_FUSED_EXP & 2)) dq_help(t_lo);
     vm_wait<0>();
     __syncthreads();  // also: every wave is done with the LDS before the next item's DMA
-    if (leader) {
+    if (threadIdx.x == 0) {
       __hip_atomic_store(flg + t_lo * FLAG_STRIDE, j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (OWLK_FUSED_DEQ_PF) {
         int nc = -1, nj = 0;
