@@ -21,6 +21,18 @@ DEV float rb(float x) {
   return __uint_as_float(u & 0xFFFF0000u);
 }
 DEV float bf2f(bf16 x) { return (float)x; }
+// the same rounding for a PAIR by one v_cvt_pk_bf16_f32 (RNE): the packed word (bits 15:0 = a, 31:16 =
+// b, the layout of a bf16 vector store) and the two rounded values read back by integer ops, which
+// the compiler cannot fold into the neighbouring float arithmetic.  ~1.5 VALU per value against 4
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+DEV unsigned cvt2(float a, float b) {
+  const bf16x2 v = {(bf16)a, (bf16)b};
+  unsigned w = __builtin_bit_cast(unsigned, v);
+  __asm__("" : "+v"(w));  // one conversion of the pair (seen through, hipcc splits it into two plus shifts)
+  return w;
+}
+DEV float bf_lo(unsigned w) { return __uint_as_float(w << 16); }
+DEV float bf_hi(unsigned w) { return __uint_as_float(w & 0xFFFF0000u); }
 // lanes of one wave handing values to each other through LDS (a staging image written by some lanes,
 // read back by others): the compiler's memory model is per thread, so without this it may reorder a
 // lane's reads above its own writes when it proves their addresses differ.  Emits no instruction.

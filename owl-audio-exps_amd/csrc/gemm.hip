@@ -56,6 +56,9 @@ struct GemmP {
 };
 
 constexpr int FRAME_ROWS = 64;  // rows per frame of a frame-strided operand (OWLK_FRAME_ROWS)
+#ifndef OWLK_GEMM_EPI2  // 1: gemm_pp_kernel's epilogue in paired-rounding form (epi_apply2); 0: epi_apply
+#define OWLK_GEMM_EPI2 1
+#endif
 
 // element offset of row r: plain (F = false) or frame-strided
 template <bool F>
@@ -334,6 +337,101 @@ DEV void epi_apply(const GemmP& p, long z, long gm, long gn, float (&v)[8], cons
     }
     st_nt((bf16x8*)((bf16*)p.C + z * p.sC + gm * p.ldc + gn), pack8(y));
     st_nt((bf16x8*)(p.aux + z * p.sAux + gm * p.ldaux + gn), pack8(o));
+  }
+}
+
+// epi_apply in paired form (OWLK_GEMM_EPI2): every bf16 rounding of two neighbouring values is one
+// v_cvt_pk_bf16_f32 whose packed word is also what gets stored (the integer rb() costs 4 VALU per value;
+// the SiLU / dSiLU / gate epilogues ran 2,000-3,200 instructions per wave and tile, now 1,600-2,900:
+// -2..4 % per GEMM, profiles/r5i_gemm_epi_ab.txt).  Same operations in the same order as epi_apply,
+// bit-identical outputs (tools/gemm_epi_bench.py --compare).  The
+// caller passes element offsets of this row chunk in C (c), aux (ao) and resid (ro), formed from per-lane
+// bases plus wave-uniform row steps; x / g are the aux-or-resid and gate inputs it loaded.
+template <int EPI, bool OF32>
+DEV void epi_apply2(const GemmP& p, long c, long ao, long ro, float (&v)[8], const float (&bb)[8],
+                    const bf16x8& x, const bf16x8& g, float (&cs)[8]) {
+  const u32x4 xw = __builtin_bit_cast(u32x4, x), gw = __builtin_bit_cast(u32x4, g);
+  u32x4 o, y;
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
+    if (OF32) {
+      float* C = (float*)p.C + c;
+      if (p.beta != 0.f) {
+        const f32x4 o0 = *(const f32x4*)C, o1 = *(const f32x4*)(C + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += p.beta * o0[e];
+          v[e + 4] += p.beta * o1[e];
+        }
+      }
+      *(f32x4*)C = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(C + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      bf16* C = (bf16*)p.C + c;
+      if (p.beta != 0.f) {
+        float ob[8];
+        unpack8(*(const bf16x8*)C, ob);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += p.beta * ob[e];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = cvt2(v[2 * k], v[2 * k + 1]);
+      st_nt((bf16x8*)C, __builtin_bit_cast(bf16x8, o));
+    }
+  } else if (EPI == EPI_SILU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      y[k] = cvt2(v[2 * k] + bb[2 * k], v[2 * k + 1] + bb[2 * k + 1]);
+      o[k] = cvt2(silu_f(bf_lo(y[k])), silu_f(bf_hi(y[k])));
+    }
+    st_nt((bf16x8*)(p.aux + ao), __builtin_bit_cast(bf16x8, y));
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, o));
+  } else if (EPI == EPI_GATE_RESID) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      y[k] = cvt2(v[2 * k] + bb[2 * k], v[2 * k + 1] + bb[2 * k + 1]);
+      const unsigned t = cvt2(bf_lo(gw[k]) * bf_lo(y[k]), bf_hi(gw[k]) * bf_hi(y[k]));
+      o[k] = cvt2(bf_lo(xw[k]) + bf_lo(t), bf_hi(xw[k]) + bf_hi(t));
+    }
+    if (p.aux) st_nt((bf16x8*)(p.aux + ao), __builtin_bit_cast(bf16x8, y));
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, o));
+  } else if (EPI == EPI_DSILU) {
+    u32x4 a;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned rv = cvt2(v[2 * k], v[2 * k + 1]);
+      float ov[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float xx = h ? bf_hi(xw[k]) : bf_lo(xw[k]);
+        const float sg = sigmoid_f(xx);
+        ov[h] = (h ? bf_hi(rv) : bf_lo(rv)) * sg * (1.f + xx * (1.f - sg));
+      }
+      o[k] = cvt2(ov[0], ov[1]);
+      a[k] = cvt2(silu_f(bf_lo(xw[k])), silu_f(bf_hi(xw[k])));  // stored only with p.resid (no branch per word)
+      cs[2 * k] += bf_lo(o[k]);  // unconditional (a select per value otherwise); used only with p.colsum
+      cs[2 * k + 1] += bf_hi(o[k]);
+    }
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, o));
+    if (p.resid) st_nt((bf16x8*)((bf16*)p.resid + ro), __builtin_bit_cast(bf16x8, a));
+  } else if (EPI == EPI_AXPBY) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned r = cvt2(v[2 * k], v[2 * k + 1]);
+      const unsigned s1 = cvt2(p.alpha * bf_lo(r), p.alpha * bf_hi(r));
+      const unsigned s2 = cvt2(p.beta * bf_lo(xw[k]), p.beta * bf_hi(xw[k]));
+      o[k] = cvt2(bf_lo(s1) + bf_lo(s2), bf_hi(s1) + bf_hi(s2));
+    }
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, o));
+  } else if (EPI == EPI_SCALE2) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      y[k] = cvt2(v[2 * k], v[2 * k + 1]);
+      o[k] = cvt2(p.alpha * bf_lo(y[k]), p.alpha * bf_hi(y[k]));
+    }
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, y));
+    st_nt((bf16x8*)(p.aux + ao), __builtin_bit_cast(bf16x8, o));
   }
 }
 
@@ -808,12 +906,26 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
   // prefetch depth (strips): every input of the tile up front where registers allow
   constexpr int PD = (EPI == EPI_DSILU || EPI == EPI_AXPBY) ? 8 : (EPI == EPI_GATE_RESID ? 4 : 1);
   bf16x8 xin[8][2], gin[8][2];  // [strip][q]
+  // OWLK_GEMM_EPI2: per-lane element offsets of row wrow0 + (lane >> 3) in C / aux / resid; the row
+  // chunks of the tile are wave-uniform steps d = 16 i + 8 q from them (frame-strided C: the chunk
+  // stays inside the lane's 64-row frame block, as wrow0 % 128 == 0 and (d & 63) + 7 < 64)
+  const int l8 = lane >> 3;
+  const bool full = m0 + 256 <= p.M;
+  const long cbase = z * p.sC + row_off<FC>(wrow0 + l8, p.ldc, p.c_fs) + gn;
+  const long abase = z * p.sAux + (wrow0 + l8) * p.ldaux + gn;
+  const long rbase0 = z * p.sRes + (wrow0 + l8) * p.ldres + gn;
+  auto c_step = [&](int d) { return FC ? (long)(d >> 6) * p.c_fs + (long)(d & 63) * p.ldc : (long)d * p.ldc; };
   auto load_in = [&](int i, bf16x8 (&x)[2], bf16x8 (&g)[2]) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       long gm = wrow0 + 16 * i + 8 * q + (lane >> 3);
       gm = gm < p.M ? gm : p.M - 1;
-      if (HAS_X) {
+      if (HAS_X && OWLK_GEMM_EPI2) {
+        const int d = 16 * i + 8 * q;
+        const long xo = EPI == EPI_GATE_RESID ? (full ? rbase0 + d * p.ldres : z * p.sRes + gm * p.ldres + gn)
+                                              : (full ? abase + d * p.ldaux : z * p.sAux + gm * p.ldaux + gn);
+        x[q] = *(const bf16x8*)((EPI == EPI_GATE_RESID ? p.resid : p.aux) + xo);
+      } else if (HAS_X) {
         const bf16* src = EPI == EPI_GATE_RESID ? p.resid + z * p.sRes + gm * p.ldres
                                                  : p.aux + z * p.sAux + gm * p.ldaux;
         x[q] = *(const bf16x8*)(src + gn);
@@ -867,7 +979,14 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
           v[e] = lo[e];
           v[e + 4] = hi[e];
         }
-        if (gm < p.M) epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
+        if (OWLK_GEMM_EPI2) {
+          const int d = 16 * i + 8 * q;
+          if (gm < p.M)
+            epi_apply2<EPI, OF32>(p, cbase + c_step(d), abase + d * p.ldaux, rbase0 + d * p.ldres, v, bb, xin[i][q],
+                                  gin[i][q], cs);
+        } else if (gm < p.M) {
+          epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
