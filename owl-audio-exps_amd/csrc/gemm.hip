@@ -1400,6 +1400,12 @@ static bool fits256(long M, long N, long K, int a_trans, int b_trans, int c_f32,
   return use256 && K % 64 == 0 && N % 256 == 0 && (!a_trans || M % 256 == 0) && (!b_trans || N % 256 == 0) &&
          !(c_f32 && beta != 0.f && beta != 1.f);
 }
+// fewest 256^2 tiles that take the ping-pong kernel (one partial round of 256 CUs beats 3+ rounds of the
+// 128^2 kernel: the per-frame modulation GEMM [1,536 x 9,216 x 1,536] has 216); OWLK_GEMM_MIN256 for A/B
+static long min_tiles256() {
+  static const long v = getenv("OWLK_GEMM_MIN256") ? atol(getenv("OWLK_GEMM_MIN256")) : 192;
+  return v;
+}
 // Skinny-M GEMMs (decode: one 64-token frame against the full weights) give few 64x64 tiles; split K
 // so the grid streams the weights from every CU: bf16 output with STORE (beta 0) / SILU / GATE_RESID
 // epilogues, applied after a fixed-order reduce of the fp32 partials (deterministic).
@@ -1427,13 +1433,14 @@ enum SplitKind { SPLIT_NONE = 0, SPLIT_SKINNY, SPLIT_256, SPLIT_128, SPLIT_DECOD
 struct SplitPlan {
   int kind;
   long splits, kchunk;
+  bool opt = false;  // taken only with a workspace (deterministic partials); else the unsplit plan
 };
 
 // frames: frame-strided operand rows (owlk_gemm_frames) -- only the 256^2 kernel reads them, so
 // neither the decode plan nor the skinny split-K plan may be taken
 static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta, bool frames = false) {
-  SplitPlan pl{SPLIT_NONE, 1, K};
+  SplitPlan pl{SPLIT_NONE, 1, K, false};
   static const int use_decode = getenv("OWLK_GEMM_DECODE") ? atoi(getenv("OWLK_GEMM_DECODE")) : 1;
   if (use_decode && !frames && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_T == 0 && K % 32 == 0 &&
       ((M + DEC_T - 1) / DEC_T) * (N / DEC_T) <= kDecodeCounterBytes / 4 &&
@@ -1462,7 +1469,24 @@ static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int
         return pl;
       }
     }
-    if (tiles256 >= 256) return pl;
+    if (c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && K < 16384 &&
+        tiles256 < 128) {
+      // few tiles, mid K (the per-frame cond gradient [1,536 x 1,536 x 9,216]: 108 -> 62 us): one round
+      // of 256^2 splits of >= 1,024 instead of the 128^2 kernel's two, with a workspace only (without:
+      // the unsplit plan, deterministic, rather than fp32 atomics).  At K = 1,536 (the modulation
+      // weight gradients) the same plan measured equal ([3,072 x 1,536]) or slower ([1,536 x 1,536]:
+      // 25 -> 34 us) than the 64^2 kernel (profiles/r5w_small_gemm_ab.txt)
+      long sp = 256 / tiles256;
+      if (sp > K / 1024) sp = K / 1024;
+      if (sp > 1) {
+        pl.kchunk = chunk(sp);
+        pl.splits = (K + pl.kchunk - 1) / pl.kchunk;
+        pl.kind = SPLIT_256;
+        pl.opt = true;
+        return pl;
+      }
+    }
+    if (tiles256 >= min_tiles256()) return pl;
   }
   if (c_f32 && epi == EPI_STORE && (beta == 1.f || (beta == 0.f && batch == 1)) && K >= 8192 && tiles128 < 1024) {
     long sp = (1024 + tiles128 - 1) / tiles128;
@@ -1525,9 +1549,11 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   p.kchunk = K;
   const bool frames = p.a_fs || p.b_fs || p.c_fs;
-  const SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta, frames);
+  SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta, frames);
   const long pws = split_ws_bytes(pl, M, N, batch);
   const bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
+  static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
+  if (pl.opt && (!have_ws || atomic_splitk)) pl = SplitPlan{SPLIT_NONE, 1, K, false};
   if (pl.kind == SPLIT_DECODE && (pl.splits == 1 || have_ws)) return launch_decode(p, epi, ws, s);
   {
     const long sk = pl.splits;
@@ -1548,7 +1574,6 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   // split-K onto an fp32 output: partials into the caller's workspace + one fixed-order reduce
   // (any beta, deterministic); without a large enough workspace (or OWLK_GEMM_ATOMIC=1) fp32
   // atomics onto C, cleared first when beta = 0
-  static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
   OWLK_REQUIRE(!frames || (fits256(M, N, K, a_trans, b_trans, c_f32, beta) && batch == 1 &&
                            (pl.kind == SPLIT_256 || pl.kind == SPLIT_NONE) &&
                            (pl.kind != SPLIT_256 || (have_ws && !atomic_splitk)) && pl.kchunk % FRAME_ROWS == 0),
@@ -1574,7 +1599,7 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
         return owlk::check_launch("splitk_reduce");
       }
     }
-    if (tiles256 >= 256) return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
+    if (tiles256 >= min_tiles256()) return dispatch256(p, a_trans, b_trans, epi, c_f32, batch, s);
   }
   // long reductions onto small outputs (weight gradients, K = tokens) that do not tile by 256:
   // 128x128 tiles, K split so the grid covers ~4 workgroups per CU; per-split partials + a

@@ -83,6 +83,20 @@ def main():
                                                   resid=act4, colsum=cs), 4 * d, d),
         ("fc2 dX plain", lambda: K.gemm(x, w2, b_trans=True, out=out4), 4 * d, d),
     ]
+    # the per-frame modulation GEMM of every block (F = 1,536 frames x 6d outputs)
+    cf, wm, bm = r(T // 64, d), r(6 * d, d) * 0.05, torch.randn(6 * d, device=dev) * 0.1
+    modo = torch.empty(T // 64, 6 * d, device=dev, dtype=torch.bfloat16)
+    cases.append(("modulation fwd", lambda: K.gemm(cf, wm, bias=bm, out=modo), 6 * d, d))
+    # d cond += d mods [F x 6d] . Wmod [6d x d] (fp32 accumulate, beta 1)
+    dmod, cg = r(T // 64, 6 * d), torch.zeros(T // 64, d, device=dev)
+    cases.append(("cond grad", lambda: K.gemm(dmod, wm, b_trans=True, out=cg, out_f32=True, beta=1.0), d, 6 * d))
+    # modulation weight gradients dW [2d | d x d] += dmods^T . s over the F frames (fp32, beta 1)
+    s_ = r(T // 64, d)
+    dw2, dw1 = torch.zeros(2 * d, d, device=dev), torch.zeros(d, d, device=dev)
+    cases.append(("mod wgrad 2d", lambda: K.gemm(dmod[:, :2 * d], s_, a_trans=True, b_trans=True, out=dw2, out_f32=True,
+                                                 beta=1.0), d, T // 64))
+    cases.append(("mod wgrad d", lambda: K.gemm(dmod[:, :d], s_, a_trans=True, b_trans=True, out=dw1, out_f32=True,
+                                                beta=1.0), d, T // 64))
     for name, fn, N, Kd in cases:
         for _ in range(2):
             fn()
@@ -94,7 +108,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.iters
-        print(f"{name:24s} [{T}x{N}x{Kd}] {ms:7.3f} ms {2.0 * T * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
+        Mr = {"modulation fwd": T // 64, "cond grad": T // 64, "mod wgrad 2d": 2 * d, "mod wgrad d": d}.get(name, T)
+        print(f"{name:24s} [{Mr}x{N}x{Kd}] {ms:7.3f} ms {2.0 * Mr * N * Kd / ms / 1e9:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
