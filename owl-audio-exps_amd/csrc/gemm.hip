@@ -1059,10 +1059,11 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
   static const int pp = getenv("OWLK_GEMM_PP") ? atoi(getenv("OWLK_GEMM_PP")) : 1;
   static const int fuse_cs = getenv("OWLK_GEMM_COLSUM") ? atoi(getenv("OWLK_GEMM_COLSUM")) : 1;
   if (pp && EPI == EPI_DSILU && batch == 1 && fuse_cs) p.colsum = p.colsum_req;
-  // grouped tile order for the short-K GEMMs (K <= 2048: -2..4 % at dit_v4's K = 1536 shapes);
-  // at K >= 4608 and for split-K weight gradients row-major order measured equal or better
+  // grouped tile order for the short-K GEMMs (K <= 4096: -2..4 % at dit_v4's K = 1536 shapes, -2..6 %
+  // at dit_v4_5B's K = 2560, profiles/r5z_gemm_group_5b_ab.txt); at K >= 4608 and for split-K weight
+  // gradients row-major order measured equal or better
   static const int group_m = getenv("OWLK_GEMM_GROUP") ? atoi(getenv("OWLK_GEMM_GROUP")) : -1;
-  p.group_m = group_m >= 0 ? group_m : (splits == 1 && p.kchunk <= 2048 ? 4 : 0);
+  p.group_m = group_m >= 0 ? group_m : (splits == 1 && p.kchunk <= 4096 ? 4 : 0);
   const int fs = (p.a_fs ? 1 : 0) | (p.b_fs ? 2 : 0) | (p.c_fs ? 4 : 0);
   if (fs) {
     // frame-strided rows: only the combinations the MMDiT block uses are built

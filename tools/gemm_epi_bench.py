@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--save")
     ap.add_argument("--compare", nargs=2)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--d", type=int, default=1536, help="model width (dit_v4_5B: 2560)")
     args = ap.parse_args()
     if args.compare:
         sys.exit(1 if compare(*args.compare) else 0)
@@ -65,7 +66,7 @@ def main():
         torch.save({k: v.cpu() for k, v in out.items()}, args.save)
         print(f"saved {len(out)} outputs to {args.save}")
 
-    T, d = 98304, 1536
+    T, d = 98304, args.d
     x, h = r(T, d), r(T, 4 * d)
     w1, w2, wq, wo = r(4 * d, d) * 0.05, r(d, 4 * d) * 0.05, r(3 * d, d) * 0.05, r(d, d) * 0.05
     b1, b2 = torch.randn(4 * d, device=dev) * 0.1, torch.randn(d, device=dev) * 0.1
