@@ -1,5 +1,5 @@
 # Step-level interleaved A/B on one box: round-3 attention tile changes off (OWLK_DQ_NT=2 OWLK_FWD_KT128=0
-# OWLK_FWD_NQ3=0 OWLK_BWD_QT2_MIN=1000000000) vs the defaults.  usage: bash tools/r3_step_ab.sh [config]
+# OWLK_FWD_NQ3=0 OWLK_BWD_QT2_MIN=1000000000) vs the defaults.  usage: bash tools/runs/r3_step_ab.sh [config]
 set -e
 cd "$GRAFT_REPO_ROOT"
 CFG=${1:-configs/dit_v4.yml}
