@@ -22,3 +22,6 @@ for k, d in tot.items():
     print("   per SIMD: mfma util %.3f  valu issue %.3f  salu issue %.3f  waves/SIMD %.2f  lds util %.3f" % (
         d["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / cyc, d["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / cyc,
         d["SQ_ACTIVE_INST_SCA"] * 4 / 1024 / cyc, W * 4 / 1024 / cyc, d["SQ_LDS_IDX_ACTIVE"] / 256 / cyc))
+    if d.get("SQ_LDS_IDX_ACTIVE"):
+        print("   lds bank conflict / active %.3f   trans VALU / VALU %.3f" % (
+            d.get("SQ_LDS_BANK_CONFLICT", 0) / d["SQ_LDS_IDX_ACTIVE"], d.get("SQ_INSTS_VALU_TRANS_F", 0) / max(d["SQ_INSTS_VALU"], 1)))
