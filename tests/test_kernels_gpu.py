@@ -53,11 +53,13 @@ def test_gemm_layouts(M, N, K_, at, bt):
     assert rel(outb, ref) < 5e-3
 
 
-@pytest.mark.parametrize("K_", [64, 128, 192, 1536])
+@pytest.mark.parametrize("K_", [64, 128, 192, 1536, 2560, 4096])
 @pytest.mark.parametrize("at,bt", [(False, False), (False, True), (True, True), (True, False)])
 def test_gemm256_pingpong(K_, at, bt):
     """>= 256 tiles of 256^2 route to the ping-pong LDS-DMA kernel: K-tile counts 1, 2, 3 (ring
-    prologue / drain edge cases) and 24, every operand layout, rows clamped on a ragged M."""
+    prologue / drain edge cases) and 24, every operand layout, rows clamped on a ragged M; K 2560 and
+    4096 take the grouped tile order (groups of 4 tile rows, 17 rows on the ragged M: a last group
+    of one)."""
     M, N = 4096 + (0 if at else 40), 4096
     A = rnd(K_, M, seed=11) if at else rnd(M, K_, seed=11)
     B = rnd(K_, N, seed=12) if bt else rnd(N, K_, seed=12)
