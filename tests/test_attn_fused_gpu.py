@@ -98,7 +98,9 @@ FUSED_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 5])  # write-through, XCD-local, XCD-local one chain at a time
+# write-through, XCD-local, XCD-local one chain at a time; bit 7: one wave per SIMD (attn_bwd_fused4.hip,
+# the hand-placed main step)
+@pytest.mark.parametrize("variant", [0, 1, 5, 128, 129])
 @pytest.mark.parametrize("case", FUSED_CASES)
 def test_attention_bwd_fused_vs_oracle_and_split(case, variant, monkeypatch):
     k = K()
@@ -162,7 +164,8 @@ def test_attention_bwd_fused_timeout_poisons_dq(variant_env, monkeypatch):
 def test_attention_bwd_fused_deterministic(case):
     """Every query tile receives its key blocks' dQ parts in key-block order, so two runs -- and the
     write-through and the XCD-local hand-offs, which differ only in where the sums live, and the
-    chain-group dequeue orders (variant bits 2-5) -- give the same bits."""
+    chain-group dequeue orders (variant bits 2-5) -- give the same bits.  So does the one-wave-per-SIMD
+    kernel (bit 7): its hand-placed step forms every product in the 8-wave kernel's order."""
     k = K()
     B, H, nf, tpf, causal, window = case
     D, L = 64, nf * tpf
@@ -171,7 +174,7 @@ def test_attention_bwd_fused_deterministic(case):
     o, lse = k.attn_fwd(q, kk, v, H, D, mask)
     delta = _delta(o, do, H, D)
     runs = []
-    for variant in (0, 0, 1, 1, 5, 9):
+    for variant in (0, 0, 1, 1, 5, 9, 128, 129, 133):
         g = [torch.full_like(q, float("nan")) for _ in range(3)]
         ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *g, D ** -0.5, variant)
         torch.cuda.synchronize()
@@ -182,7 +185,7 @@ def test_attention_bwd_fused_deterministic(case):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 7])
+@pytest.mark.parametrize("variant", [2, 3, 7, 131])
 @pytest.mark.parametrize("shape", [(1, 24, 1536, 64, True, None), (2, 3, 20, 64, True, None), (1, 1, 300, 1, True, None),
                                    (1, 2, 40, 64, False, None), (1, 8, 96, 65, True, None),
                                    (1, 24, 1536, 64, True, 16), (1, 2, 30, 65, True, 4), (1, 2, 40, 64, False, 3),
@@ -243,7 +246,7 @@ DOC_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 5, 129])
 @pytest.mark.parametrize("case", DOC_CASES)
 def test_attention_bwd_fused_packed_documents(case, variant, monkeypatch):
     """Causal masks of packed documents (kv_lo / q_hi, the runs form): the single pass against the
