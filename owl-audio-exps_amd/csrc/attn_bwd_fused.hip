@@ -889,7 +889,8 @@ extern "C" int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void
   int dev = 0;
   (void)hipGetDevice(&dev);
   // variant bit 7: one wave per SIMD (attn_bwd_fused4_k, the hand-placed main step)
-  const bool w4 = (variant & 128) != 0;
+  // (its bf16 dQ rows are stored through a buffer resource: L * lddq * 2 must stay below 2^31)
+  const bool w4 = (variant & 128) != 0 && L * lddq * 2 < (1L << 31);
   const dim3 grid((unsigned)fused_grid(dev, w4));
   // the XCD-local hand-off only on an 8-XCC device (else: write-through)
   if ((variant & 1) && !all_xcds_present(dev)) variant &= ~1;

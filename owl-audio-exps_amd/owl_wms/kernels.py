@@ -430,6 +430,9 @@ def _bwd_side_stream(device, D, mask):
     return s
 
 
+FUSED_FAIL_TEST = False
+
+
 def fused_bwd_variant(D, mask):
     """owlk_attn_bwd_fused variant for this layer, or None for the two-kernel backward.  The single
     pass serves head_dim 64 with a document-free mask, windowed or not (dit_v4's layers), and causal
@@ -451,9 +454,11 @@ def fused_bwd_variant(D, mask):
     # one at a time (default) gives each chain the XCD's 32 workgroups: -2 % time and -54 % HBM
     # traffic against all three of dit_v4's at once (profiles/r4j_ab.log)
     group = int(os.environ.get("OWLK_BWD_FUSED_GROUP", "1"))
-    # OWLK_BWD_FUSED_FAIL_TEST = 1 (tests only, variant bit 6): chain 0's block-1 hand-off waits time
-    # out, so the error path -- the error word and NaN dQ rows -- is exercised through this entry
-    fail = 64 if os.environ.get("OWLK_BWD_FUSED_FAIL_TEST") == "1" else 0
+    # FUSED_FAIL_TEST (tests only, set through monkeypatch; variant bit 6): chain 0's block-1 hand-off
+    # waits time out, so the error path -- the error word and NaN dQ rows -- is exercised through
+    # this entry.  A module attribute, not an environment variable: one left exported would turn
+    # every training step's dQ into NaN
+    fail = 64 if FUSED_FAIL_TEST else 0
     return (1 if env == "2" else 0) | (group & 15) << 2 | fail
 
 

@@ -143,7 +143,7 @@ def test_attention_bwd_fused_timeout_poisons_dq(variant_env, monkeypatch):
     mask = k.FrameMask(tpf, None, True)
     o, lse = k.attn_fwd(q, kk, v, H, D, mask)
     monkeypatch.setenv("OWLK_BWD_FUSED", variant_env)
-    monkeypatch.setenv("OWLK_BWD_FUSED_FAIL_TEST", "1")
+    monkeypatch.setattr(k, "FUSED_FAIL_TEST", True)
     dq, dk, dv = (torch.zeros_like(q) for _ in range(3))
     k.attn_bwd(q, kk, v, o, do, lse, H, D, mask, dq, dk, dv)
     torch.cuda.synchronize()

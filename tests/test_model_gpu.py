@@ -575,11 +575,12 @@ def test_device_state_decode_matches_host_state(d_model):
 
 
 def test_fused_handoff_timeout_reaches_the_loss(monkeypatch):
-    """A timed-out dQ hand-off of the single-pass backward (forced: OWLK_BWD_FUSED_FAIL_TEST, variant
+    """A timed-out dQ hand-off of the single-pass backward (forced: kernels.FUSED_FAIL_TEST, variant
     bit 6) is not a silent wrong gradient: the qkv weight gradients come out non-finite, and after one
     Muon / AdamW step (rft_trainer.py:186-199's consumer of the gradients) the next loss is NaN."""
+    from owl_wms import kernels
     from owl_wms.muon import init_muon
-    monkeypatch.setenv("OWLK_BWD_FUSED_FAIL_TEST", "1")
+    monkeypatch.setattr(kernels, "FUSED_FAIL_TEST", True)
     m, d = _run("bf16")
     assert torch.isfinite(d["diffusion_loss"]).item()  # the forward is untouched
     bad = [k for k, p in m.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
@@ -588,7 +589,7 @@ def test_fused_handoff_timeout_reaches_the_loss(monkeypatch):
                     adamw_betas=[0.9, 0.95], adamw_keys=["core.proj_in", "core.proj_out.proj", "core.t_embed",
                                                          "core.control_embed", "gate", "adaln"])
     opt.step()
-    monkeypatch.delenv("OWLK_BWD_FUSED_FAIL_TEST")
+    monkeypatch.setattr(kernels, "FUSED_FAIL_TEST", False)
     m.zero_grad(set_to_none=True)
     d2 = m(GR["gamerft.bf16.in.x"].cuda(), GR["gamerft.bf16.in.mouse"].cuda(), GR["gamerft.bf16.in.btn"].cuda(),
            GR["gamerft.bf16.in.doc_id"].cuda(), return_dict=True)

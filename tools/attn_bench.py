@@ -115,8 +115,8 @@ def main():
             err = hw[8].item()
             pw = ws[128:256].view(torch.int64).cpu().tolist()
             if any(pw):  # OWLK_FUSED_PROF builds: cycles per phase, dQ waves | other waves
-                names = ("dq", "main", "vmwait", "barrier", "dequeue", "prologue", "epilogue")
-                for nm, part in (("dQ waves", pw[:7]), ("other waves", pw[8:15])):
+                names = ("dq", "main", "vmwait", "barrier", "dequeue", "prologue", "epilogue", "dq2")
+                for nm, part in (("dQ waves", pw[:8]), ("other waves", pw[8:16])):
                     tot = sum(part) or 1
                     print(f"  fused phases, {nm} (s_memtime cycles, share of the workgroup time): " +
                           ", ".join(f"{n} {v / tot:.3f}" for n, v in zip(names, part)) +

@@ -17,7 +17,7 @@ between them at a fixed place:
 * the -dS rows into the [key][query] LDS image right after their packing;
 * the transposed dO^T / Q^T fragments of the dV / dK products.
 
-Registers are fixed here, not by hipcc: the statement clobbers v[96:255] and a[192:255]; the
+Registers are fixed here, not by hipcc: the statement clobbers v[112:255] and the AGPR file; the
 accumulators dK^T / dV^T and the K' / V' fragments are compiler-allocated AGPR operands (they
 stay in a[0:191]).  The generator counts every LDS operation (in-order completion; lgkmcnt is
 4 bits, so counts above 15 over-wait) and pads the MFMA hazards with s_nop:
@@ -33,14 +33,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "owl-audio-exps_amd", "csrc", "attn_bwd_fused4_step.inc")
 
 TILE_BYTES = 64 * 128
+VLO = 96  # the statement's VGPRs: v[VLO:255]
 FQT = 64
 MF = "v_mfma_f32_16x16x32_bf16"
 
 
 class Ins:
-    __slots__ = ("text", "kind", "reads", "writes", "lds", "cost", "mfma_c")
+    __slots__ = ("text", "kind", "reads", "writes", "lds", "cost", "mfma_c", "passes")
 
-    def __init__(self, text, kind, reads=(), writes=(), lds=False, cost=4, mfma_c=()):
+    def __init__(self, text, kind, reads=(), writes=(), lds=False, cost=4, mfma_c=(), passes=4):
         self.text = text
         self.kind = kind  # mfma | valu | exp | ldsr | ldsw | cmp | nop | wait | salu
         self.reads = list(reads)  # physical registers ('v', n) / ('a', n)
@@ -48,6 +49,7 @@ class Ins:
         self.lds = lds
         self.cost = cost
         self.mfma_c = list(mfma_c)  # registers read as the accumulator input (chain)
+        self.passes = passes
 
 
 def vr(lo, n):
@@ -72,12 +74,12 @@ def DP(h, t4, qs):
     return 128 + 64 * h + 32 + 8 * t4 + 4 * qs
 
 
-def LR(h, qs):  # lse2 rows (the S chain's initial value)
-    return 96 + 16 * h + 4 * qs
+def LR(h, qs):  # lse2 rows (the S chain's initial value); half 1's reuse half 0's registers
+    return 112 + 4 * qs
 
 
 def DR(h, qs):  # delta rows
-    return 96 + 16 * h + 8 + 4 * qs
+    return 112 + 8 + 4 * qs
 
 
 # Persistent AGPRs (the whole work item; only this file's statements touch the AGPR file, the
@@ -109,10 +111,31 @@ def TQ(h, ds):
     return (216 + 8 * ds) if h == 0 else (192, 200, 208, 248)[ds]
 
 
-def build(masked):
-    """Program order of one step: list of Ins (operand names in %[...])."""
-    pro = []  # before MFMA 0
-    mf = []  # 128 MFMAs
+QA = 96  # the dQ^T accumulator (32 d x 32 q, v_mfma_f32_32x32x16_bf16): v[96:111]
+MF32 = "v_mfma_f32_32x32x16_bf16"
+
+
+def DQR(s):  # dQ operand ring (4 slots x 8): K^T fragment +0..3, dS^T fragment +4..7; tq_0's registers
+    return 216 + 8 * s
+
+
+def stamp(i):
+    return Ins(f"s_memtime %[ts{i}]", "raw")
+
+
+RING_SLOT = 2 * TILE_BYTES + 2 * FQT * 4
+DS_BYTES = 256 * 128
+
+
+def build(kind, local, prof=False, P=0):
+    """Program order of one step: list of Ins (operand names in %[...]).  kind: 'full', 'masked' (PARTIAL
+    tiles: the allowed query range of each key applied after the exponentials) or 'empty' (no key of
+    the wave sees the tile: only the dQ products, zero -dS rows, the stores and the check)."""
+    masked = kind == "masked"
+    SL = P * RING_SLOT  # this tile's ring slot (t & 1 = P), the next tile's DMA goes to the other
+    SN = (1 - P) * RING_SLOT
+    pro = []  # before the first MFMA
+    mf = []  # 128 16x16x32 MFMAs
     # ---- MFMA stream
     # M1_h: for ks, qs, t4: S, dP  (group (ks, qs) = ring group 4h + 2ks + qs)
     for h in range(2):
@@ -141,35 +164,59 @@ def build(masked):
                 mf.append(Ins(f"{MF} {rng('a', DK(i), 4)}, {rng('a', tq + 4, 4)}, {rng('v', sf, 4)}, {rng('a', DK(i), 4)}",
                               "mfma", reads=ar(tq + 4, 4) + vr(sf, 4) + ar(DK(i), 4), writes=ar(DK(i), 4), mfma_c=ar(DK(i), 4)))
     assert len(mf) == 128
+    # the previous tile's dQ^T[32 d x 32 q] += K^T[32 d x 16 keys] dS^T[16 keys x 32 q] over the item's
+    # 256 keys (attn_bwd_fused_k's dq_mfma, same order): 16 MFMAs, one between every two of M1_0's
+    dq = []
+    for k2 in range(16):
+        r = DQR(k2 % 4)
+        dq.append(Ins(f"{MF32} {rng('v', QA, 16)}, {rng('a', r, 4)}, {rng('a', r + 4, 4)}, {rng('v', QA, 16)}", "mfma",
+                      reads=ar(r, 8) + vr(QA, 16), writes=vr(QA, 16), mfma_c=vr(QA, 16), passes=8))
+    stream = []  # (Ins, small index or None)
+    for i in range(128):
+        if i < 32 and i % 2 == 0:
+            stream.append((dq[i // 2], None))
+        stream.append((mf[i], i))
+    pos = {i: n for n, (_, i) in enumerate(stream) if i is not None}
+    dpos = [n for n, (x, i) in enumerate(stream) if i is None]
 
     # ---- LDS reads
     def rd_group(g):  # Q row fragment (A of S) and dO row fragment (A of dP) of ring group g
         h, ks, qs = g // 4, (g // 2) & 1, g & 1
         row = 32 * h + 16 * qs
         slot = RING(g % 3)
-        return [Ins(f"ds_read_b128 {rng('a', slot, 4)}, %[ar{ks}] offset:{128 * row}", "ldsr", writes=ar(slot, 4), lds=True),
-                Ins(f"ds_read_b128 {rng('a', slot + 4, 4)}, %[ar{ks}] offset:{TILE_BYTES + 128 * row}", "ldsr",
+        return [Ins(f"ds_read_b128 {rng('a', slot, 4)}, %[ar{ks}] offset:{SL + 128 * row}", "ldsr", writes=ar(slot, 4), lds=True),
+                Ins(f"ds_read_b128 {rng('a', slot + 4, 4)}, %[ar{ks}] offset:{SL + TILE_BYTES + 128 * row}", "ldsr",
                     writes=ar(slot + 4, 4), lds=True)]
 
     def rd_rows(h):
         out = []
         for qs in range(2):
             row = 32 * h + 16 * qs
-            out.append(Ins(f"ds_read_b128 {rng('v', LR(h, qs), 4)}, %[al] offset:{2 * TILE_BYTES + 4 * row}", "ldsr",
+            out.append(Ins(f"ds_read_b128 {rng('v', LR(h, qs), 4)}, %[al] offset:{SL + 2 * TILE_BYTES + 4 * row}", "ldsr",
                            writes=vr(LR(h, qs), 4), lds=True))
-            out.append(Ins(f"ds_read_b128 {rng('v', DR(h, qs), 4)}, %[al] offset:{2 * TILE_BYTES + 4 * FQT + 4 * row}",
+            out.append(Ins(f"ds_read_b128 {rng('v', DR(h, qs), 4)}, %[al] offset:{SL + 2 * TILE_BYTES + 4 * FQT + 4 * row}",
                            "ldsr", writes=vr(DR(h, qs), 4), lds=True))
         return out
 
     def rd_tr(h, ds):  # dO^T (A of dV^T) and Q^T (A of dK^T) of column group ds, permuted k order
         tq = TQ(h, ds)
-        o = 4096 * h
+        o = SL + 4096 * h
         return [Ins(f"ds_read_b64_tr_b16 {rng('a', tq, 2)}, %[tr{ds}] offset:{TILE_BYTES + o}", "ldsr", writes=ar(tq, 2), lds=True),
                 Ins(f"ds_read_b64_tr_b16 {rng('a', tq + 2, 2)}, %[tr{ds}] offset:{TILE_BYTES + o + 2048}", "ldsr",
                     writes=ar(tq + 2, 2), lds=True),
                 Ins(f"ds_read_b64_tr_b16 {rng('a', tq + 4, 2)}, %[tr{ds}] offset:{o}", "ldsr", writes=ar(tq + 4, 2), lds=True),
                 Ins(f"ds_read_b64_tr_b16 {rng('a', tq + 6, 2)}, %[tr{ds}] offset:{o + 2048}", "ldsr",
                     writes=ar(tq + 6, 2), lds=True)]
+
+    def rd_dq(k2):  # K^T (image rows 16 k2 ..) and dS^T fragments of dQ k-step k2 (frag_tr of attn_bwd_fused_k)
+        r = DQR(k2 % 4)
+        # (the dS image of tile t + 1: the other one)
+        return [Ins(f"ds_read_b64_tr_b16 {rng('a', r + 2 * i, 2)}, %[{nm}] offset:{2048 * k2 + (i // 2) * (1 - P) * DS_BYTES}",
+                    "ldsr", writes=ar(r + 2 * i, 2), lds=True) for i, nm in enumerate(("ka", "kb", "sa", "sb"))]
+
+    def rd_qacc():  # the dQ sum so far (predecessor's, zeros or NaN), lane-linear in the landing zone
+        return [Ins(f"ds_read_b128 {rng('v', QA + 4 * e, 4)}, %[qa] offset:{1024 * e}", "ldsr", writes=vr(QA + 4 * e, 4),
+                    lds=True) for e in range(4)]
 
     # ---- softmax-gradient VALU of (h, t4), then its two -dS row writes
     def chunk(h, t4):
@@ -199,26 +246,110 @@ def build(masked):
                 out.append(Ins(f"v_cvt_pk_bf16_f32 v{base + wd}, v{base + 2 * wd}, v{base + 2 * wd + 1}", "valu",
                                reads=vr(base + 2 * wd, 2), writes=vr(base + wd, 1)))
         # -dS rows of keys 16 t4 + c into the image: queries 32 h + 4 g .. (e 0), 32 h + 16 + 4 g .. (e 1)
-        out.append(Ins(f"ds_write_b64 %[ds{2 * h}], {rng('v', dp0, 2)} offset:{2048 * t4}", "ldsw", reads=vr(dp0, 2), lds=True,
-                       cost=8))
-        out.append(Ins(f"ds_write_b64 %[ds{2 * h + 1}], {rng('v', dp0 + 2, 2)} offset:{2048 * t4}", "ldsw",
+        out.append(Ins(f"ds_write_b64 %[ds{2 * h}], {rng('v', dp0, 2)} offset:{P * DS_BYTES + 2048 * t4}", "ldsw",
+                       reads=vr(dp0, 2), lds=True, cost=8))
+        out.append(Ins(f"ds_write_b64 %[ds{2 * h + 1}], {rng('v', dp0 + 2, 2)} offset:{P * DS_BYTES + 2048 * t4}", "ldsw",
                        reads=vr(dp0 + 2, 2), lds=True, cost=8))
         return out
 
-    # ---- placement: fillers[i] = instructions issued right before MFMA i
-    fill = [[] for _ in range(129)]
-    # prologue: rows and ring groups 0, 1 of half 0
-    pro += rd_rows(0)[0:2] + rd_group(0) + rd_rows(0)[2:4] + rd_group(1)
+    # ---- the dQ stores (after the last dQ MFMA): mode 0 = the fp32 sum (4 x 16 B per lane into the
+    # chain's accumulator, lane-linear; write-through unless local), 1 = the tile's last contributor's
+    # bf16 dQ rows (-scale folded in; 4 x 8 B per lane, rows past L addressed out of the buffer's range)
+    def stores():
+        pol = "" if local else " sc1"
+        t = ["s_bitcmp1_b32 %[fl], 0", "s_cbranch_scc1 .Lf4bf%="]
+        t += [f"buffer_store_dwordx4 {rng('v', QA + 4 * e, 4)}, %[soffa], %[rsrc], %[soffs] offen offset:{1024 * e}{pol}"
+              for e in range(4)]
+        t += ["s_branch .Lf4st%=", ".Lf4bf%=:"]
+        t += [f"v_mul_f32_e32 v{QA + i}, %[nscale], v{QA + i}" for i in range(16)]
+        t += [f"v_cvt_pk_bf16_f32 v{QA + i}, v{QA + 2 * i}, v{QA + 2 * i + 1}" for i in range(8)]
+        t += [f"buffer_store_dwordx2 {rng('v', QA + 2 * rr, 2)}, %[soffr], %[rsrc], %[soffs] offen offset:{16 * rr}"
+              for rr in range(4)]
+        t += [".Lf4st%=:"]
+        return [Ins("\n".join(t), "raw", reads=vr(QA, 16), writes=vr(QA, 16))]
+
+    # ---- the hand-off check of the tile this step sweeps: its flag (polled by LDS-DMA before the
+    # statement) against want (INT_MAX when the tile has no predecessor to wait for); on a match the predecessor's sum goes to the landing zone (4 LDS-DMA
+    # pieces, sc1), to be consumed by the next step.  The dQ stores are the 4 youngest vector-memory
+    # operations here, so vmcnt(4) waits for the poll (and the ring's DMA, issued before it)
+    def check():
+        tmp = LR(0, 0)
+        out = [Ins("s_waitcnt vmcnt(4)", "raw"),
+               Ins(f"ds_read_b32 v{tmp}, %[flagv]", "ldsr", writes=vr(tmp, 1), lds=True),
+               Ins(f"v_readfirstlane_b32 %[tmp], v{tmp}", "valu", reads=vr(tmp, 1))]
+        t = ["s_nop 3", "s_mov_b32 %[lout], 0",
+             "s_cmp_lt_i32 %[tmp], %[want]", "s_cbranch_scc1 .Lf4np%=", "s_mov_b32 %[lout], 1",
+             "s_mov_b32 m0, %[m0a]", "s_nop 0"]
+        t += [f"global_load_lds_dwordx4 %[soffa], %[sumbase] offset:{1024 * e} sc1" for e in range(4)]
+        t += [".Lf4np%=:"]
+        out.append(Ins("\n".join(t), "raw"))
+        return out
+
+    # the flag of this step's tile, polled by LDS-DMA (sc1) at the statement's top: every lane loads the
+    # word into its slot of the wave's flag area; checked at the top of M2_0
+    poll = [Ins("s_mov_b32 m0, %[m0f]\ns_nop 0\nglobal_load_lds_dword %[zero], %[fb] sc1", "raw")]
+
+    # the ring's LDS-DMA of the next tile (t - 1, into the other slot): 2 Q + 2 dO rows-pieces per wave
+    # (rows 16 w + 8 h ..), the lse2 (wave 0) / delta (wave 1) row; flags bit 1 / bit 2
+    def dma_piece(i):
+        if i < 4:
+            src, off = ("qb", f"qo{i % 2}") if i < 2 else ("ob", f"oo{i % 2}")
+            dst = SN + (TILE_BYTES if i >= 2 else 0) + 1024 * (i % 2)
+            t = ["s_bitcmp1_b32 %[fl], 1", f"s_cbranch_scc0 .Lf4d{i}%=", f"s_add_u32 m0, %[m0q], {dst}", "s_nop 0",
+                 f"global_load_lds_dwordx4 %[{off}], %[{src}]", f".Lf4d{i}%=:"]
+        else:
+            t = ["s_bitcmp1_b32 %[fl], 2", f"s_cbranch_scc0 .Lf4d{i}%=", f"s_add_u32 m0, %[m0l], {SN}", "s_nop 0",
+                 "global_load_lds_dword %[lo], %[lb]", f".Lf4d{i}%=:"]
+        return Ins("\n".join(t), "raw")
+
+    if kind == "empty":
+        zero = [Ins("v_mov_b32 v112, 0", "valu", writes=vr(112, 1)), Ins("v_mov_b32 v113, 0", "valu", writes=vr(113, 1))]
+        zero += [Ins(f"ds_write_b64 %[ds{i}], v[112:113] offset:{P * DS_BYTES + 2048 * t4}", "ldsw", reads=vr(112, 2), lds=True)
+                 for t4 in range(4) for i in range(4)]
+        fill = [[] for _ in range(17)]
+        for k2 in range(13):
+            fill[k2 + 1] += rd_dq(k2 + 3)
+        fill[1] += zero[:2]
+        for n in range(8):
+            fill[n + 1] += zero[2 + 2 * n:4 + 2 * n]
+        for i in range(5):
+            fill[2 + 2 * i].append(dma_piece(i))
+        prog = [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_nop 3", "nop")] + poll + rd_qacc() + rd_dq(0) + rd_dq(1) + rd_dq(2)
+        for n in range(16):
+            prog += fill[n]
+            prog.append(dq[n])
+        prog += fill[16] + stores() + check()
+        return prog
+
+    # ---- placement: fill[n] = instructions issued right before stream entry n
+    N = len(stream)
+    fill = [[] for _ in range(N + 1)]
+    # prologue: the dQ sum, dQ k-step 0, rows and ring group 0 of half 0, k-step 1, ring group 1, k-step 2
+    pro += rd_qacc() + rd_dq(0) + rd_rows(0)[0:2] + rd_group(0) + rd_rows(0)[2:4] + rd_dq(1) + rd_group(1) + rd_dq(2)
+    # dQ k-step k2 + 3 right after dQ MFMA k2 (4-slot ring)
+    for k2 in range(13):
+        fill[dpos[k2] + 1] += rd_dq(k2 + 3)
     # ring groups 2 .. 7, two groups ahead of their first MFMA (group g's MFMAs are 8 g .. 8 g + 7)
     for g in range(2, 8):
-        fill[8 * (g - 2) + 1] += rd_group(g)
-    # lse2 / delta rows of half 1 (for MFMA 32)
-    fill[13] += rd_rows(1)
-    # dO^T / Q^T of half 0 (first use MFMA 64) during M1_1; of half 1 (ring registers, free after
-    # MFMA 63) during M2_0 (first use 96)
+        fill[pos[8 * (g - 2) + 1]] += rd_group(g)
+    # lse2 / delta rows of half 1 (for MFMA 32), into half 0's row registers once its chains have
+    # read them (MFMAs 0 .. 15)
+    fill[pos[19]] += rd_rows(1)
+    # the dQ stores after M1_0 (12 wait states after the last 32x32x16 MFMA, padded by finalize)
+    fill[pos[32]] += stores()
+    # dO^T / Q^T of half 0 (first use MFMA 64) during M1_1, in the dQ ring's registers (free after M1_0);
+    # of half 1 (ring registers, free after MFMA 63) during M2_0 (first use 96)
     for ds in range(4):
-        fill[36 + 6 * ds] += rd_tr(0, ds)
-        fill[66 + 6 * ds] += rd_tr(1, ds)
+        fill[pos[36 + 6 * ds]] += rd_tr(0, ds)
+        fill[pos[66 + 6 * ds]] += rd_tr(1, ds)
+    # the hand-off check at the top of M2_0 (the landing zone's loads then have half a step)
+    fill[pos[64]] = check() + fill[pos[64]]
+    for i in range(5):  # the ring's DMA between the MFMAs of M1_0 + dQ (no VALU there)
+        fill[pos[3 + 4 * i]].append(dma_piece(i))
+    if prof:  # s_memtime at the block boundaries (SMEM: one outstanding keeps every lgkmcnt wait safe)
+        fill[pos[32]].append(stamp(1))
+        fill[pos[64]].insert(0, stamp(2))
+        fill[pos[96]].insert(0, stamp(3))
     # VALU: half 0 chunks paced over MFMAs 33 .., half 1 after; chunk (h, t4) due before MFMA 64 + 32 h + 8 t4
     vstream = []
     for h in range(2):
@@ -234,13 +365,15 @@ def build(masked):
             gap = lo_gap + (k * (hi_gap - lo_gap)) // total
             gap = max(gap, first)
             gap = min(gap, due)
-            fill[gap].append(x)
+            fill[pos[gap]].append(x)
             k += 1
-    prog = [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_nop 3", "nop")] + pro
-    for i in range(128):
-        prog += fill[i]
-        prog.append(mf[i])
-    prog += fill[128]
+    prog = [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_nop 3", "nop")] + ([stamp(0)] if prof else []) + poll + pro
+    for n in range(N):
+        prog += fill[n]
+        prog.append(stream[n][0])
+    prog += fill[N]
+    if prof:
+        prog += [stamp(4), Ins("s_waitcnt lgkmcnt(0)", "wait")]
     return prog
 
 
@@ -291,13 +424,13 @@ def finalize(prog):
         pad = 0
         if ins.kind == "mfma":
             for r in ins.reads:
-                if r in ins.mfma_c and last_w.get(r, (-99, ""))[1] == "mfma":
+                if r in ins.mfma_c and last_w.get(r, (-99, "", 0))[1] == "mfma":
                     continue  # accumulate chain
                 w = last_w.get(r)
                 if w and w[1] in ("valu", "exp"):
                     pad = max(pad, 2 - ws_since(w[0]))
                 if w and w[1] == "mfma":
-                    pad = max(pad, 10 - ws_since(w[0]))
+                    pad = max(pad, w[2] + 4 - ws_since(w[0]))
             for r in ins.writes:
                 w = last_w.get(r)
                 if w and w[1] in ("valu", "exp"):
@@ -306,7 +439,7 @@ def finalize(prog):
             for r in ins.reads:
                 w = last_w.get(r)
                 if w and w[1] == "mfma":
-                    pad = max(pad, 8 - ws_since(w[0]))
+                    pad = max(pad, w[2] - ws_since(w[0]))
             for r in ins.writes:
                 m = last_mfma.get(r)
                 if m is not None:
@@ -320,8 +453,8 @@ def finalize(prog):
             pos += n
             pad -= n
             nops += 1
-        # 3. issue
-        out.append(ins.text)
+        # 3. issue (a raw block -- branches, stores -- counts as one wait state: its shortest path)
+        out += ins.text.split("\n")
         if ins.lds:
             idx = issued
             issued += 1
@@ -329,7 +462,8 @@ def finalize(prog):
                 for r in ins.writes:
                     pending[r] = idx
         for r in ins.writes:
-            last_w[r] = (pos, "mfma" if ins.kind == "mfma" else ("ld" if ins.kind == "ldsr" else "valu"))
+            last_w[r] = (pos, "mfma" if ins.kind == "mfma" else ("ld" if ins.kind == "ldsr" else "valu"),
+                         12 if ins.passes == 8 else 8)
         if ins.kind == "mfma":
             for r in ins.mfma_c + ins.writes:
                 last_mfma[r] = pos
@@ -345,34 +479,53 @@ def finalize(prog):
     return out, dict(nops=nops, waits=waits, instrs=len(out))
 
 
-def operand_decl(masked):
-    outs = []
-    ins = ['[ar0] "v"(ar0)', '[ar1] "v"(ar1)', '[al] "v"(al)'] + [f'[tr{i}] "v"(tr[{i}])' for i in range(4)]
-    ins += [f'[ds{i}] "v"(dsa[{i}])' for i in range(4)]
+VOPS = ["ar0", "ar1", "al", "tr0", "tr1", "tr2", "tr3", "ds0", "ds1", "ds2", "ds3", "qa", "ka", "kb", "sa", "sb", "soffa",
+        "soffr", "flagv", "qo0", "qo1", "oo0", "oo1", "lo", "zero"]
+SOPS = [("rsrc", "__amdgpu_buffer_rsrc_t"), ("fl", "int"), ("nscale", "float"), ("want", "int"), ("soffs", "int"),
+        ("sumbase", "const void*"), ("m0a", "unsigned"), ("m0f", "unsigned"), ("m0q", "unsigned"), ("m0l", "unsigned"),
+        ("qb", "const void*"), ("ob", "const void*"), ("lb", "const void*"), ("fb", "const void*")]
+
+
+def operand_decl(kind, prof=False):
+    masked = kind == "masked"
+    outs = ['[lout] "=&s"(lout)', '[tmp] "=&s"(tmp)']
+    if prof:
+        outs += [f'[ts{i}] "=&s"(ts[{i}])' for i in range(5)]
+    ins = []
+    for n in VOPS:
+        fld = f"{n[:-1]}[{n[-1]}]" if n[:-1] in ("tr", "ds", "qo", "oo") else n
+        fld = {"ds": "dsa"}.get(fld.split("[")[0], fld.split("[")[0]) + (fld[fld.index("["):] if "[" in fld else "")
+        ins.append(f'[{n}] "v"(f.{fld})')
+    ins += [f'[{n}] "s"(s.{n})' for n, _ in SOPS]
     if masked:
-        ins += [f'[mlo{i}] "v"(mlo[{i}])' for i in range(4)] + [f'[mhi{i}] "v"(mhi[{i}])' for i in range(4)]
-    clob = ['"memory"'] + [f'"v{i}"' for i in range(96, 256)] + [f'"a{i}"' for i in range(256)]
+        ins += [f'[mlo{i}] "v"(f.mlo[{i}])' for i in range(4)] + [f'[mhi{i}] "v"(f.mhi[{i}])' for i in range(4)]
+    clob = ['"memory"', '"m0"', '"scc"'] + [f'"v{i}"' for i in range(VLO, 256)] + [f'"a{i}"' for i in range(256)]
     if masked:
         clob.append('"vcc"')
     return outs, ins, clob
 
 
-def emit_function(name, masked):
-    prog = build(masked)
-    lines, st = finalize(prog)
-    outs, ins, clob = operand_decl(masked)
-    mparams = ", const int (&mlo)[4], const int (&mhi)[4]" if masked else ""
-    body = "\n".join(f'      "{l}\\n"' for l in lines)
-    s = f"""// {name}: {st['instrs']} instructions, 128 MFMAs, {st['waits']} lgkmcnt waits, {st['nops']} hazard nops
-__attribute__((always_inline)) DEV void {name}(unsigned ar0, unsigned ar1, unsigned al, const unsigned (&tr)[4],
-    const unsigned (&dsa)[4]{mparams}) {{
+def emit_function(name, kind, local, P):
+    out = []
+    for prof in (True, False):
+        prog = build(kind, local, prof and kind != "empty", P)
+        lines, st = finalize(prog)
+        outs, ins, clob = operand_decl(kind, prof and kind != "empty")
+        body = "\n".join(f'      "{l}\\n"' for l in lines)
+        out.append(f"""// {name}: {st['instrs']} lines, {st['waits']} lgkmcnt waits, {st['nops']} hazard nops; returns whether the
+// landing zone's 4 loads were issued (they are the youngest vector-memory operations then)
+__attribute__((always_inline)) DEV int {name}(const F4Lane& f, const F4Scalar& s, unsigned long long (&ts)[5]) {{
+  int lout, tmp;
   asm volatile(
 {body}
       : {", ".join(outs)}
       : {", ".join(ins)}
       : {", ".join(clob)});
+  return lout;
 }}
-"""
+""")
+    s = ("#if OWLK_FUSED_PROF  // timing-only builds: s_memtime at the MFMA-block boundaries\n" + out[0] +
+         "#else\n" + out[1] + "#endif\n")
     return s, st
 
 
@@ -408,17 +561,51 @@ def main():
     ap.add_argument("--stats", action="store_true")
     args = ap.parse_args()
     parts = []
-    for name, masked in (("fused4_main_full", False), ("fused4_main_masked", True)):
-        s, st = emit_function(name, masked)
-        print(f"{name}: {st}", file=sys.stderr)
-        parts.append(s)
+    for kind in ("full", "masked", "empty"):
+        for local in (True, False):
+            for P in (0, 1):
+                name = f"fused4_step_{kind}_{'local' if local else 'wt'}_p{P}"
+                s, st = emit_function(name, kind, local, P)
+                print(f"{name}: {st}", file=sys.stderr)
+                parts.append(s)
+    disp = ["// the statement of a step: tile kind (TILE_FULL / TILE_PARTIAL / TILE_EMPTY), hand-off form, ring parity",
+            "template <int KIND, bool LOCAL>",
+            "__attribute__((always_inline)) DEV int fused4_step(int parity, const F4Lane& f, const F4Scalar& s,",
+            "                                                 unsigned long long (&ts)[5]) {"]
+    for kind, kv in (("full", "TILE_FULL"), ("masked", "TILE_PARTIAL"), ("empty", "TILE_EMPTY")):
+        for local in (True, False):
+            nm = f"fused4_step_{kind}_{'local' if local else 'wt'}"
+            disp.append(f"  if constexpr (KIND == {kv} && {'LOCAL' if local else '!LOCAL'})")
+            disp.append(f"    return parity ? {nm}_p1(f, s, ts) : {nm}_p0(f, s, ts);")
+    disp += ["  return 0;", "}", ""]
     if args.stats:
         return
-    hdr = ("// GENERATED by tools/gen_fused4_asm.py -- do not edit.  The hand-placed main step of\n"
+    hdr = ("// GENERATED by tools/gen_fused4_asm.py -- do not edit.  The hand-placed step of\n"
            "// attn_bwd_fused4_k (attn_bwd_fused4.hip): see the generator's docstring for the schedule.\n"
-           "#pragma once\n\n")
+           "#pragma once\n\n"
+           "// per-lane operands (VGPR; constant per item): LDS byte addresses of the Q / dO row reads (ks 0 / 1),\n"
+           "// the lse2 / delta rows, the dO^T / Q^T reads, the -dS rows (slot / image 0: the other parity is an\n"
+           "// immediate), the landing zone, the K^T and dS^T reads of dQ; dQ store offsets (fp32 sum / bf16 rows),\n"
+           "// the polled flag; the ring DMA's source offsets (Q / dO rows h, lse2 or delta); a zero\n"
+           "struct F4Lane {\n"
+           "  unsigned ar0, ar1, al, tr[4], dsa[4], qa, ka, kb, sa, sb, soffa, soffr, flagv, qo[2], oo[2], lo, zero;\n"
+           "  int mlo[4], mhi[4];  // PARTIAL tiles: allowed query rows per key tile, relative to the tile, - 4 g\n"
+           "};\n"
+           "// wave-uniform operands (SGPR): the dQ store target (accumulator / dq rows / none) with flags bit 0 =\n"
+           "// bf16 rows (the tile's last contributor), bit 1 = issue the ring's DMA, bit 2 = the lse2 / delta\n"
+           "// piece; -scale; the check's want (INT_MAX: no check); the stores' soffset; the tile's sum in the\n"
+           "// workspace; M0 bases (landing zone, flag area, ring rows of this wave, lse2 / delta row); DMA sources\n"
+           "struct F4Scalar {\n"
+           "  __amdgpu_buffer_rsrc_t rsrc;\n"
+           "  int fl;\n"
+           "  float nscale;\n"
+           "  int want, soffs;\n"
+           "  const void* sumbase;\n"
+           "  unsigned m0a, m0f, m0q, m0l;\n"
+           "  const void *qb, *ob, *lb, *fb;\n"
+           "};\n\n")
     with open(OUT, "w") as f:
-        f.write(hdr + emit_helpers() + "\n" + "\n".join(parts))
+        f.write(hdr + emit_helpers() + "\n" + "\n".join(parts) + "\n" + "\n".join(disp))
     print("wrote", OUT, file=sys.stderr)
 
 
