@@ -454,12 +454,17 @@ def fused_bwd_variant(D, mask):
     # one at a time (default) gives each chain the XCD's 32 workgroups: -2 % time and -54 % HBM
     # traffic against all three of dit_v4's at once (profiles/r4j_ab.log)
     group = int(os.environ.get("OWLK_BWD_FUSED_GROUP", "1"))
+    # OWLK_BWD_FUSED_W4 (variant bit 7): the one-wave-per-SIMD kernel with the hand-placed step
+    # (attn_bwd_fused4.hip) -- "global" (default): layers without a window (its per-item fixed cost
+    # loses on the short sweeps of windowed layers), "1": every layer, "0": none
+    w4env = os.environ.get("OWLK_BWD_FUSED_W4", "global")
+    w4 = 128 if (w4env == "1" or (w4env == "global" and mask.window is None)) else 0
     # FUSED_FAIL_TEST (tests only, set through monkeypatch; variant bit 6): chain 0's block-1 hand-off
     # waits time out, so the error path -- the error word and NaN dQ rows -- is exercised through
     # this entry.  A module attribute, not an environment variable: one left exported would turn
     # every training step's dQ into NaN
     fail = 64 if FUSED_FAIL_TEST else 0
-    return (1 if env == "2" else 0) | (group & 15) << 2 | fail
+    return (1 if env == "2" else 0) | (group & 15) << 2 | fail | w4
 
 
 def attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, variant=0, ws=None):

@@ -31,6 +31,11 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "owl-audio-exps_amd", "csrc", "attn_bwd_fused4_step.inc")
+# schedule knobs for A/B builds (tools/build_f4_variants.sh): the 16x16x32 MFMA the hand-off check goes
+# before, the first MFMA of the ring DMA pieces and their spacing
+KNOB = {k: int(os.environ.get("F4_" + k.upper(), v))
+        for k, v in (("check", 96), ("dma0", 3), ("dmastep", 4), ("pro", 0), ("dqslots", 4), ("xnodma", 0),
+                     ("xnodqr", 0))}  # x*: timing-only experiments (results wrong)
 
 TILE_BYTES = 64 * 128
 VLO = 96  # the statement's VGPRs: v[VLO:255]
@@ -115,8 +120,8 @@ QA = 96  # the dQ^T accumulator (32 d x 32 q, v_mfma_f32_32x32x16_bf16): v[96:11
 MF32 = "v_mfma_f32_32x32x16_bf16"
 
 
-def DQR(s):  # dQ operand ring (4 slots x 8): K^T fragment +0..3, dS^T fragment +4..7; tq_0's registers
-    return 216 + 8 * s
+def DQR(s):  # dQ operand ring (4 or 5 slots x 8): K^T fragment +0..3, dS^T fragment +4..7; tq_0's
+    return (216, 224, 232, 240, 248)[s]  # registers (+ tq_1's last group), free until M1_1
 
 
 def stamp(i):
@@ -167,13 +172,14 @@ def build(kind, local, prof=False, P=0):
     # the previous tile's dQ^T[32 d x 32 q] += K^T[32 d x 16 keys] dS^T[16 keys x 32 q] over the item's
     # 256 keys (attn_bwd_fused_k's dq_mfma, same order): 16 MFMAs, one between every two of M1_0's
     dq = []
+    NS = KNOB["dqslots"]
     for k2 in range(16):
-        r = DQR(k2 % 4)
+        r = DQR(k2 % NS)
         dq.append(Ins(f"{MF32} {rng('v', QA, 16)}, {rng('a', r, 4)}, {rng('a', r + 4, 4)}, {rng('v', QA, 16)}", "mfma",
                       reads=ar(r, 8) + vr(QA, 16), writes=vr(QA, 16), mfma_c=vr(QA, 16), passes=8))
     stream = []  # (Ins, small index or None)
     for i in range(128):
-        if i < 32 and i % 2 == 0:
+        if i < 32 and i % 2 == KNOB["pro"]:
             stream.append((dq[i // 2], None))
         stream.append((mf[i], i))
     pos = {i: n for n, (_, i) in enumerate(stream) if i is not None}
@@ -209,7 +215,7 @@ def build(kind, local, prof=False, P=0):
                     writes=ar(tq + 6, 2), lds=True)]
 
     def rd_dq(k2):  # K^T (image rows 16 k2 ..) and dS^T fragments of dQ k-step k2 (frag_tr of attn_bwd_fused_k)
-        r = DQR(k2 % 4)
+        r = DQR(k2 % NS)
         # (the dS image of tile t + 1: the other one)
         return [Ins(f"ds_read_b64_tr_b16 {rng('a', r + 2 * i, 2)}, %[{nm}] offset:{2048 * k2 + (i // 2) * (1 - P) * DS_BYTES}",
                     "ldsr", writes=ar(r + 2 * i, 2), lds=True) for i, nm in enumerate(("ka", "kb", "sa", "sb"))]
@@ -292,6 +298,8 @@ def build(kind, local, prof=False, P=0):
     # the ring's LDS-DMA of the next tile (t - 1, into the other slot): 2 Q + 2 dO rows-pieces per wave
     # (rows 16 w + 8 h ..), the lse2 (wave 0) / delta (wave 1) row; flags bit 1 / bit 2
     def dma_piece(i):
+        if KNOB["xnodma"]:
+            return Ins("s_nop 0", "raw")
         if i < 4:
             src, off = ("qb", f"qo{i % 2}") if i < 2 else ("ob", f"oo{i % 2}")
             dst = SN + (TILE_BYTES if i >= 2 else 0) + 1024 * (i % 2)
@@ -325,10 +333,17 @@ def build(kind, local, prof=False, P=0):
     N = len(stream)
     fill = [[] for _ in range(N + 1)]
     # prologue: the dQ sum, dQ k-step 0, rows and ring group 0 of half 0, k-step 1, ring group 1, k-step 2
-    pro += rd_qacc() + rd_dq(0) + rd_rows(0)[0:2] + rd_group(0) + rd_rows(0)[2:4] + rd_dq(1) + rd_group(1) + rd_dq(2)
-    # dQ k-step k2 + 3 right after dQ MFMA k2 (4-slot ring)
-    for k2 in range(13):
-        fill[dpos[k2] + 1] += rd_dq(k2 + 3)
+    # (pro 1: the first S / dP operands first, and the stream opens with two 16x16x32 MFMAs)
+    ahead = NS - 1
+    if KNOB["pro"]:
+        pro += rd_rows(0)[0:2] + rd_group(0) + rd_qacc() + rd_dq(0) + rd_rows(0)[2:4] + rd_group(1)
+        pro += sum((rd_dq(k) for k in range(1, ahead)), [])
+    else:
+        pro += rd_qacc() + rd_dq(0) + rd_rows(0)[0:2] + rd_group(0) + rd_rows(0)[2:4] + rd_dq(1) + rd_group(1)
+        pro += sum((rd_dq(k) for k in range(2, ahead)), [])
+    # dQ k-step k2 + NS - 1 right after dQ MFMA k2 (NS-slot ring)
+    for k2 in range(16 - ahead):
+        fill[dpos[k2] + 1] += rd_dq(k2 + ahead)
     # ring groups 2 .. 7, two groups ahead of their first MFMA (group g's MFMAs are 8 g .. 8 g + 7)
     for g in range(2, 8):
         fill[pos[8 * (g - 2) + 1]] += rd_group(g)
@@ -343,12 +358,12 @@ def build(kind, local, prof=False, P=0):
         fill[pos[36 + 6 * ds]] += rd_tr(0, ds)
         fill[pos[66 + 6 * ds]] += rd_tr(1, ds)
     # the hand-off check at the top of M2_0 (the landing zone's loads then have half a step)
-    fill[pos[64]] = check() + fill[pos[64]]
+    fill[pos[KNOB["check"]]] = check() + fill[pos[KNOB["check"]]]
     for i in range(5):  # the ring's DMA between the MFMAs of M1_0 + dQ (no VALU there)
-        fill[pos[3 + 4 * i]].append(dma_piece(i))
+        fill[pos[KNOB["dma0"] + KNOB["dmastep"] * i]].append(dma_piece(i))
     if prof:  # s_memtime at the block boundaries (SMEM: one outstanding keeps every lgkmcnt wait safe)
         fill[pos[32]].append(stamp(1))
-        fill[pos[64]].insert(0, stamp(2))
+        fill[pos[64]].insert(0, stamp(2))  # (after a check placed at 64)
         fill[pos[96]].insert(0, stamp(3))
     # VALU: half 0 chunks paced over MFMAs 33 .., half 1 after; chunk (h, t4) due before MFMA 64 + 32 h + 8 t4
     vstream = []
