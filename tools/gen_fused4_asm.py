@@ -35,7 +35,7 @@ OUT = os.path.join(REPO, "owl-audio-exps_amd", "csrc", "attn_bwd_fused4_step.inc
 # before, the first MFMA of the ring DMA pieces and their spacing
 KNOB = {k: int(os.environ.get("F4_" + k.upper(), v))
         for k, v in (("check", 96), ("dma0", 3), ("dmastep", 4), ("pro", 0), ("dqslots", 4), ("xnodma", 0),
-                     ("xnodqr", 0))}  # x*: timing-only experiments (results wrong)
+                     ("xnodqr", 0), ("ringv", 0), ("rvl", 49))}  # x*: timing-only experiments (results wrong)
 
 TILE_BYTES = 64 * 128
 VLO = 96  # the statement's VGPRs: v[VLO:255]
@@ -278,9 +278,16 @@ def build(kind, local, prof=False, P=0):
     # statement) against want (INT_MAX when the tile has no predecessor to wait for); on a match the predecessor's sum goes to the landing zone (4 LDS-DMA
     # pieces, sc1), to be consumed by the next step.  The dQ stores are the 4 youngest vector-memory
     # operations here, so vmcnt(4) waits for the poll (and the ring's DMA, issued before it)
-    def check():
+    def check(ringw=False):
         tmp = LR(0, 0)
-        out = [Ins("s_waitcnt vmcnt(4)", "raw"),
+        out = [Ins("s_waitcnt vmcnt(4)", "raw")]
+        if ringw:  # the next tile's ring rows, staged in v[112:127] / v96 since rvl, into the other slot
+            t = ["s_waitcnt vmcnt(0)", "s_bitcmp1_b32 %[fl], 1", "s_cbranch_scc0 .Lf4rw%="]
+            t += [f"ds_write_b128 %[rq], {rng('v', 112 + 4 * i, 4)} offset:{SN + (TILE_BYTES if i >= 2 else 0) + 1024 * (i % 2)}"
+                  for i in range(4)]
+            t += ["s_bitcmp1_b32 %[fl], 2", "s_cbranch_scc0 .Lf4rw%=", f"ds_write_b32 %[rl], v96 offset:{SN}", ".Lf4rw%=:"]
+            out = [Ins("\n".join(t), "raw", reads=vr(112, 16) + vr(96, 1))]  # (LDS ops not counted: later waits over-wait)
+        out += [
                Ins(f"ds_read_b32 v{tmp}, %[flagv]", "ldsr", writes=vr(tmp, 1), lds=True),
                Ins(f"v_readfirstlane_b32 %[tmp], v{tmp}", "valu", reads=vr(tmp, 1))]
         t = ["s_nop 3", "s_mov_b32 %[lout], 0",
@@ -357,10 +364,17 @@ def build(kind, local, prof=False, P=0):
     for ds in range(4):
         fill[pos[36 + 6 * ds]] += rd_tr(0, ds)
         fill[pos[66 + 6 * ds]] += rd_tr(1, ds)
-    # the hand-off check at the top of M2_0 (the landing zone's loads then have half a step)
-    fill[pos[KNOB["check"]]] = check() + fill[pos[KNOB["check"]]]
-    for i in range(5):  # the ring's DMA between the MFMAs of M1_0 + dQ (no VALU there)
-        fill[pos[KNOB["dma0"] + KNOB["dmastep"] * i]].append(dma_piece(i))
+    if KNOB["ringv"]:  # the ring rows by plain loads into v[112:127] (free after half 1's first chains) / v96
+        t = ["s_bitcmp1_b32 %[fl], 1", "s_cbranch_scc0 .Lf4rv%="]
+        t += [f"global_load_dwordx4 {rng('v', 112 + 4 * i, 4)}, %[{('qo', 'oo')[i // 2]}{i % 2}], %[{('qb', 'ob')[i // 2]}]"
+              for i in range(4)]
+        t += ["s_bitcmp1_b32 %[fl], 2", "s_cbranch_scc0 .Lf4rv%=", "global_load_dword v96, %[lo], %[lb]", ".Lf4rv%=:"]
+        fill[pos[KNOB["rvl"]]].append(Ins("\n".join(t), "raw", writes=vr(112, 16) + vr(96, 1)))
+        fill[pos[KNOB["check"]]] = check(True) + fill[pos[KNOB["check"]]]
+    else:
+        fill[pos[KNOB["check"]]] = check() + fill[pos[KNOB["check"]]]
+        for i in range(5):  # the ring's DMA between the MFMAs of M1_0 + dQ (no VALU there)
+            fill[pos[KNOB["dma0"] + KNOB["dmastep"] * i]].append(dma_piece(i))
     if prof:  # s_memtime at the block boundaries (SMEM: one outstanding keeps every lgkmcnt wait safe)
         fill[pos[32]].append(stamp(1))
         fill[pos[64]].insert(0, stamp(2))  # (after a check placed at 64)
@@ -495,7 +509,7 @@ def finalize(prog):
 
 
 VOPS = ["ar0", "ar1", "al", "tr0", "tr1", "tr2", "tr3", "ds0", "ds1", "ds2", "ds3", "qa", "ka", "kb", "sa", "sb", "soffa",
-        "soffr", "flagv", "qo0", "qo1", "oo0", "oo1", "lo", "zero"]
+        "soffr", "flagv", "qo0", "qo1", "oo0", "oo1", "lo", "zero", "rq", "rl"]
 SOPS = [("rsrc", "__amdgpu_buffer_rsrc_t"), ("fl", "int"), ("nscale", "float"), ("want", "int"), ("soffs", "int"),
         ("sumbase", "const void*"), ("m0a", "unsigned"), ("m0f", "unsigned"), ("m0q", "unsigned"), ("m0l", "unsigned"),
         ("qb", "const void*"), ("ob", "const void*"), ("lb", "const void*"), ("fb", "const void*")]
@@ -542,6 +556,68 @@ __attribute__((always_inline)) DEV int {name}(const F4Lane& f, const F4Scalar& s
     s = ("#if OWLK_FUSED_PROF  // timing-only builds: s_memtime at the MFMA-block boundaries\n" + out[0] +
          "#else\n" + out[1] + "#endif\n")
     return s, st
+
+
+def emit_run(local):
+    """fused4_run_<local|wt>: n steps over FULL tiles with uniform conditions (the fp32 sum as the dQ store
+    target, the ring DMA on, the predecessor check either on for every step (flags bit 3) or off) as ONE
+    statement: per step the landing zone (vmcnt wait, or zeros without a predecessor), the step body of
+    the tile's parity, the end-of-step wait, the barrier and the flag of tile t + 1, then every pointer
+    moved back one tile -- no scalar work of the compiler's between steps.  Stops before a step whose
+    predecessor's sum was not seen by the previous step's check (lout 0 with bit 3 set): the caller's
+    loop then polls.  Returns the steps left; lout = the last step's check result."""
+    bodies = {}
+    for P in (0, 1):
+        lines, st = finalize(build("full", local, False, P))
+        bodies[P] = [l.replace("%=", f"%=q{P}") for l in lines]
+    # (entry: the caller's last step left only its landing-zone loads, or none, in flight)
+    t = ["s_waitcnt vmcnt(0)", "s_cmp_eq_u32 %[par], 0", "s_cbranch_scc0 .Lf4L1%="]
+    for P in (0, 1):
+        t += [f".Lf4L{P}%=:", "s_bitcmp1_b32 %[fl], 3", f"s_cbranch_scc0 .Lf4z{P}%=",
+              "s_cmp_eq_u32 %[lout], 0", "s_cbranch_scc1 .Lf4x%=",
+              "s_waitcnt vmcnt(0)",  # the landing zone's loads
+              f"s_branch .Lf4pd{P}%=", f".Lf4z{P}%=:"]
+        t += [f"v_mov_b32 v{112 + i}, 0" for i in range(4)]
+        t += [f"ds_write_b128 %[qa], v[112:115] offset:{1024 * e}" for e in range(4)]
+        t += [f".Lf4pd{P}%=:"] + bodies[P]
+        t += ["s_cmp_eq_u32 %[lout], 0", f"s_cbranch_scc1 .Lf4v{P}%=", "s_waitcnt vmcnt(4)", f"s_branch .Lf4w{P}%=",
+              f".Lf4v{P}%=:", "s_waitcnt vmcnt(0)", f".Lf4w{P}%=:", "s_waitcnt lgkmcnt(0)", "s_barrier",
+              # lane 0 of wave 0 raises the flag of tile t + 1 (every wave's dQ stores are done)
+              "s_cmp_eq_u32 %[wid], 0", f"s_cbranch_scc0 .Lf4f{P}%=", "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
+              "global_store_dword %[zero], %[fval], %[fb] offset:64 sc1", "s_mov_b64 exec, s[78:79]", f".Lf4f{P}%=:",
+              "s_sub_u32 s64, s64, %[qstep]", "s_subb_u32 s65, s65, 0",
+              "s_sub_u32 s66, s66, %[ostep]", "s_subb_u32 s67, s67, 0",
+              "s_sub_u32 s68, s68, 256", "s_subb_u32 s69, s69, 0",
+              "s_sub_u32 s70, s70, 64", "s_subb_u32 s71, s71, 0",
+              "s_sub_u32 s72, s72, 0x4000", "s_subb_u32 s73, s73, 0",
+              "s_sub_u32 s74, s74, 0x4000",
+              "s_sub_u32 s75, s75, 1", "s_cmp_eq_u32 s75, 0", "s_cbranch_scc1 .Lf4x%="]
+        if P == 1:
+            t.append("s_branch .Lf4L0%=")
+    t.append(".Lf4x%=:")
+    outs = ['[lout] "+{s76}"(lout)', '[tmp] "=&s"(tmp)', '[n] "+{s75}"(n)', '[qb] "+{s[64:65]}"(qb)',
+            '[ob] "+{s[66:67]}"(ob)', '[lb] "+{s[68:69]}"(lb)', '[fb] "+{s[70:71]}"(fb)', '[sumbase] "+{s[72:73]}"(sumbase)',
+            '[soffs] "+{s74}"(soffs)']
+    _, ins, clob = operand_decl("full")
+    ins = [x for x in ins if not any(x.startswith(f"[{k}]") for k in ("qb", "ob", "lb", "fb", "sumbase", "soffs"))]
+    ins += ['[par] "s"(par)', '[qstep] "s"(qstep)', '[ostep] "s"(ostep)', '[fval] "v"(fval)', '[wid] "s"(wid)']
+    clob = clob + ['"s78"', '"s79"']
+    body = "\n".join(f'      "{l}\\n"' for l in t)
+    nm = f"fused4_run_{'local' if local else 'wt'}"
+    return f"""// {nm}: {len(t)} lines
+__attribute__((always_inline)) DEV int {nm}(int n, int par, int& lout, const F4Lane& f, const F4Scalar& s,
+                                            unsigned qstep, unsigned ostep, unsigned fval, int wid) {{
+  int tmp;
+  const void *qb = s.qb, *ob = s.ob, *lb = s.lb, *fb = s.fb, *sumbase = s.sumbase;
+  int soffs = s.soffs;
+  asm volatile(
+{body}
+      : {", ".join(outs)}
+      : {", ".join(ins)}
+      : {", ".join(clob)});
+  return n;
+}}
+"""
 
 
 def emit_helpers():
@@ -593,6 +669,7 @@ def main():
             disp.append(f"  if constexpr (KIND == {kv} && {'LOCAL' if local else '!LOCAL'})")
             disp.append(f"    return parity ? {nm}_p1(f, s, ts) : {nm}_p0(f, s, ts);")
     disp += ["  return 0;", "}", ""]
+    disp += ["#if !OWLK_FUSED_PROF", emit_run(True), emit_run(False), "#endif", ""]
     if args.stats:
         return
     hdr = ("// GENERATED by tools/gen_fused4_asm.py -- do not edit.  The hand-placed step of\n"
@@ -603,7 +680,7 @@ def main():
            "// immediate), the landing zone, the K^T and dS^T reads of dQ; dQ store offsets (fp32 sum / bf16 rows),\n"
            "// the polled flag; the ring DMA's source offsets (Q / dO rows h, lse2 or delta); a zero\n"
            "struct F4Lane {\n"
-           "  unsigned ar0, ar1, al, tr[4], dsa[4], qa, ka, kb, sa, sb, soffa, soffr, flagv, qo[2], oo[2], lo, zero;\n"
+           "  unsigned ar0, ar1, al, tr[4], dsa[4], qa, ka, kb, sa, sb, soffa, soffr, flagv, qo[2], oo[2], lo, zero, rq, rl;\n"
            "  int mlo[4], mhi[4];  // PARTIAL tiles: allowed query rows per key tile, relative to the tile, - 4 g\n"
            "};\n"
            "// wave-uniform operands (SGPR): the dQ store target (accumulator / dq rows / none) with flags bit 0 =\n"

@@ -1,0 +1,15 @@
+# r6q: SQ counters of the W4 global backward, per-step loop (base) vs steady-run statement (run)
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; L=$R/owl-audio-exps_amd/owl_wms/_lib
+cp $L/libowlk.so $L/libowlk_run.so
+for lib in base run; do
+for i in 1 2 3; do
+  case $i in
+    1) C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS";;
+    2) C="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC";;
+    3) C="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F SQ_ACTIVE_INST_VMEM SQ_CYCLES GRBM_GUI_ACTIVE";;
+  esac
+  OWLK_LIB=$L/libowlk_$lib.so FRAMES=1536 timeout -k 10 -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d $R/gpurun_out/pmc_$lib -f csv -o p$i -- python3 $R/tools/attn_fwd_only.py bwd > $R/gpurun_out/pmc_${lib}_$i.log 2>&1 || exit 1
+done
+done
+ls -R $R/gpurun_out/pmc_base | head -20
