@@ -105,34 +105,34 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
   const int dt32 = w & 1, qt32 = (w >> 1) & 1;
   // DQ16: this wave's quarter of dQ^T: d tile dt (16), query tiles qt0, qt0 + 1 (16 each)
   const int dt = w & 3, qt0 = 2 * (w >> 2);
-  const unsigned offk = tr16_lane_off(dt, lane), offs0 = tr16_lane_off(qt0, lane), offs1 = tr16_lane_off(qt0 + 1, lane);
+  const unsigned offk = tr16_lane_off(dt, lane), offs0 = ds_tr16_off(qt0, lane), offs1 = ds_tr16_off(qt0 + 1, lane);
   const unsigned acc_lane = (unsigned)(w * NACC * 1024 + lane * 16);  // + e * 1024, + tile * 16 KiB
   int ok32a, ok32b, os32a, os32b;
   tr32_lane_off(dt32, lane, ok32a, ok32b);
-  tr32_lane_off(qt32, lane, os32a, os32b);
+  ds_tr32_off(qt32, lane, os32a, os32b);
   // per-lane LDS byte offsets in a ring slot (row0 a multiple of 16 in the immediate): frag_row16
   // of k-step 0 / 1, frag_tr16 of column group ds, the lse2 / delta rows of lane group g
-  const unsigned ro0 = row16_lane_off(0, lane), ro1 = row16_lane_off(1, lane);
-  // dS^T image pieces (8 B): row r = 32 w + 16 t2 + c, 16-B chunk ch = 4 qb + 2 e + (g >> 1), at
-  // r * 128 + ((ch ^ swz_dual(r)) << 4) + 8 (g & 1) = dsl + 2048 t2 + ((64 qb + 32 e) ^ dsx), as
-  // swz_dual(r) = swz_dual(c) (it repeats every 16 rows) and 64 qb + 32 e has only bits 5-6
-  const unsigned dsl = (unsigned)((32 * w + c) * 128 + 8 * (g & 1));
-  const unsigned dsx = (unsigned)((((g >> 1) ^ swz_dual(c)) << 4));
-  const unsigned tro0 = tr16_lane_off(0, lane), tro1 = tr16_lane_off(1, lane), tro2 = tr16_lane_off(2, lane),
-                 tro3 = tr16_lane_off(3, lane);
+  const unsigned ro0 = ring_row16_off(0, lane), ro1 = ring_row16_off(1, lane);
+  // dS^T image pieces (8 B): row r = 32 w + 16 t2 + c, 8-B unit u = 8 qb + 4 e + g, at
+  // r * 128 + 8 (u ^ swz_ds8(r)) = dsl + 2048 t2 + ((64 qb + 32 e) ^ dsx), as swz_ds8(r) = swz_ds8(c)
+  // (it repeats every 16 rows) and 64 qb + 32 e has only bits 5-6, 8 g bits 3-4
+  const unsigned dsl = (unsigned)((32 * w + c) * 128);
+  const unsigned dsx = (unsigned)(8 * (g ^ swz_ds8(c)));
+  const unsigned tro0 = ring_tr16_off(0, lane), tro1 = ring_tr16_off(1, lane), tro2 = ring_tr16_off(2, lane),
+                 tro3 = ring_tr16_off(3, lane);
   if (blockIdx.x == 0 && threadIdx.x == 0) p.hdr[9] = FKB;  // for readers of the workspace (tests)
 
   // per-lane LDS-DMA source offsets of a 64-row tile (wave w: rows 8 w .. 8 w + 7, one 1-KiB
   // wave-instruction, swizzled source chunk)
   const int drow = 8 * w + (lane >> 3);
-  const int dch = (lane & 7) ^ swz_dual(drow);
+  const int dch = (lane & 7) ^ swz_ring(drow);
   // (formed from an opaque lane id at each use: kept live across the sweep they were spilled, and
   // each reload's vmcnt(0) drained the dQ stores before the ring's DMA)
   // OWLK_FUSED_DMA47: waves 4-7 move rows 16 (w - 4) + 8 h + (lane >> 3) instead (h = 0, 1)
   auto row_off = [&](int ld, int h = 0) {
     const int ln = (int)opaque<1>((unsigned)lane);
     const int r = OWLK_FUSED_DMA47 ? 16 * (w - 4) + 8 * h + (ln >> 3) : 8 * w + (ln >> 3);
-    return (unsigned)((r * ld + (((ln & 7) ^ swz_dual(r)) * 8)) * 2);
+    return (unsigned)((r * ld + (((ln & 7) ^ swz_ring(r)) * 8)) * 2);
   };
 
   // OWLK_FUSED_PROF: per-step phases {dq, main, vmwait, barrier} and per-item {dequeue, prologue,
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(FusedP p) {
             dma16(lds_addr(dst), Q + (long)q0 * p.ldq, row_off(p.ldq, h));
             dma16(lds_addr(dst + TILE_BYTES), dO + (long)q0 * p.ldo, row_off(p.ldo, h));
           } else {
-            const int r = 16 * (w - 4) + 8 * h + (lane >> 3), ch = (lane & 7) ^ swz_dual(r);
+            const int r = 16 * (w - 4) + 8 * h + (lane >> 3), ch = (lane & 7) ^ swz_ring(r);
             int gr = q0 + r;
             gr = gr < L ? gr : L - 1;
             dma16(lds_addr(dst), Q + (long)q0 * p.ldq, (unsigned)(((gr - q0) * p.ldq + ch * 8) * 2));

@@ -100,6 +100,37 @@ DEV unsigned tr16_lane_off(int ds, int lane) {
   return (unsigned)(x * 128 + ((ch ^ swz_dual(x)) << 4) + 8 * (c & 1));
 }
 
+// LDS swizzles of the single-pass kernels' Q / dO ring and -dS^T images, chosen against the gfx950 lane groups
+// (ds_read_b128: 4 x 16 lanes {0-3,12-15,20-27} ..; ds_write_b64: 4 x 16 contiguous lanes on 32
+// banks; ds_read_b64_tr_b16: 2 x 32) so that every ring read (row fragments and transposed), every
+// -dS row write and every dS^T read is conflict-free (swz_dual, shared with the 8-wave kernel, left
+// the ring's row reads and the -dS writes 2-way conflicted: a quarter of the LDS-array cycles).
+// Ring: 16-B chunk c of row r at c ^ (r & 6).  -dS^T image: 8-B unit u (4 queries) of key row r at
+// u ^ swz_ds8(r).  The K image keeps swz_dual (its reads are conflict-free with it).
+DEV int swz_ring(int r) { return r & 6; }
+DEV int swz_ds8(int r) { return (r & 1) | ((r & 2) << 2) | ((r & 12) >> 1); }
+DEV unsigned ring_row16_off(int ks, int lane) {  // frag_row16 of rows row0 + (lane & 15), row0 % 16 == 0
+  const int r = lane & 15;
+  return (unsigned)(r * 128 + (((4 * ks + (lane >> 4)) ^ swz_ring(r)) << 4));
+}
+DEV unsigned ring_tr16_off(int ds, int lane) {  // frag_tr16 (dO^T / Q^T) of column group ds
+  const int c = lane & 15, g = lane >> 4;
+  const int x = 4 * g + (c >> 2);
+  const int ch = 2 * ds + ((c & 3) >> 1);
+  return (unsigned)(x * 128 + ((ch ^ swz_ring(x)) << 4) + 8 * (c & 1));
+}
+DEV void ds_tr32_off(int cb, int lane, int& oa, int& ob) {  // dS^T fragment of query group cb (rows 4 h + qq, + 8)
+  const int g = lane >> 4, h = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int ra = 4 * h + qq, rb = ra + 8, u = 8 * cb + 4 * (g & 1) + pp;
+  oa = ra * 128 + 8 * (u ^ swz_ds8(ra));
+  ob = rb * 128 + 8 * (u ^ swz_ds8(rb));
+}
+DEV unsigned ds_tr16_off(int ds, int lane) {  // frag_tr16 of the dS^T image (OWLK_FUSED_DQ16; 2-way conflicted)
+  const int c = lane & 15, g = lane >> 4;
+  const int x = 4 * g + (c >> 2);
+  return (unsigned)(x * 128 + 8 * ((4 * ds + (c & 3)) ^ swz_ds8(x)));
+}
+
 // Every vector-memory access of the sweep goes through inline asm, and the waits are counted by
 // hand (vmcnt counts loads, LDS-DMA and stores in issue order).  A compiler-visible LDS-DMA makes
 // hipcc drain it (vmcnt(0)) before every ds_read_b64_tr_b16 (the builtin carries no memory operand),

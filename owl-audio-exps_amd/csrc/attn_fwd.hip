@@ -605,7 +605,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
 
-  const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_TR>(p.ldv, w, lane);
+  const GldsOff goff_k = glds_offsets<SW_ROW>(p.ldk, w, lane), goff_v = glds_offsets<SW_DUAL>(p.ldv, w, lane);
   // tile image: K [RH row halves of 64 keys][NSUB] | V [RH][NSUB]; at D 64 (NSUB 1) the RH halves of
   // K (and of V) are one contiguous 128-B-row image, and every swizzle has period 16 rows
   auto issue = [&](char* buf, long c0) {
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
           tile_glds_fast(bv, V + cr * p.ldv + 64 * sb, goff_v, w);
         } else {
           tile_glds<SW_ROW>(bk, K + 64 * sb, p.ldk, cr, p.Lkv, w, lane);
-          tile_glds<SW_TR>(bv, V + 64 * sb, p.ldv, cr, p.Lkv, w, lane);
+          tile_glds<SW_DUAL>(bv, V + 64 * sb, p.ldv, cr, p.Lkv, w, lane);
         }
       }
     }
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(FwdP p) {
         }
 #pragma unroll
         for (int ds = 0; ds < F::NDS; ++ds) {
-          const bf16x8 vt = frag_tr16<SW_TR>(lv + (ds >> 2) * SUB, 32 * kc, ds & 3, lane);
+          const bf16x8 vt = frag_tr16<SW_DUAL>(lv + (ds >> 2) * SUB, 32 * kc, ds & 3, lane);
 #pragma unroll
           for (int t4 = 0; t4 < NQ; ++t4)
             o[ds][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pf[t4], o[ds][t4], 0, 0, 0);
@@ -880,7 +880,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
 #pragma unroll
       for (int q4 = 0; q4 < KTD / 16; ++q4) {
         tile_glds<SW_ROW>(buf + sb * C::SUBK, K + 64 * sb, p.ldk, c0, p.Lkv, q4, lane);
-        tile_glds<SW_TR>(buf + (C::NSUB + sb) * C::SUBK, V + 64 * sb, p.ldv, c0, p.Lkv, q4, lane);
+        tile_glds<SW_DUAL>(buf + (C::NSUB + sb) * C::SUBK, V + 64 * sb, p.ldv, c0, p.Lkv, q4, lane);
       }
   };
   if (nt > 0) issue(0);
@@ -941,7 +941,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd16_split_k(FwdP p, const long*
       }
 #pragma unroll
       for (int ds = 0; ds < C::NDS; ++ds) {
-        const bf16x8 vt = frag_tr16<SW_TR>(lv + (ds >> 2) * C::SUBK, 32 * kc, ds & 3, lane);
+        const bf16x8 vt = frag_tr16<SW_DUAL>(lv + (ds >> 2) * C::SUBK, 32 * kc, ds & 3, lane);
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4)
           o[ds][t4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt, pf[t4], o[ds][t4], 0, 0, 0);

@@ -16,7 +16,7 @@ qkv = torch.randn(1, L, 3 * H * D, device="cuda", dtype=torch.bfloat16)
 qk = qkv[:, :, :2 * H * D].view(1, L, 2 * H, D)  # QK-RMSNorm'd, as in the model
 qk.copy_((qk.float() * torch.rsqrt(qk.float().pow(2).mean(-1, keepdim=True))).bfloat16())
 q, k, v = qkv[:, :, :H * D], qkv[:, :, H * D:2 * H * D], qkv[:, :, 2 * H * D:]
-mask = K.FrameMask(tpf, None)
+mask = K.FrameMask(tpf, int(os.environ["WINDOW"]) if os.environ.get("WINDOW") else None)
 o, lse = K.attn_fwd(q, k, v, H, D, mask, score_bound=K.qk_norm_bound(D))
 if which == "bwd":
     do = torch.randn_like(o)
