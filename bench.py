@@ -104,7 +104,7 @@ def cpu_baseline(steps=3):
 
 # kernel symbols (the 16x16x32 and 32x32x16 variants of each)
 PMC_KERNELS = {"attn_bwd_dkdv": "attn_bwd_dkdv(16)?_k", "attn_bwd_dq": "attn_bwd_dq(16)?_k", "attn_fwd": "attn_fwd",
-               "attn_bwd_fused": "attn_bwd_fused_k"}
+               "attn_bwd_fused": "attn_bwd_fused4?_k"}
 
 
 def pmc_traffic(args):
