@@ -13,6 +13,7 @@
 // lse is written in base 2 of the scaled logits, lse2 = log2 sum_k exp2(scale log2(e) s_k) (=
 // natural lse * log2 e): the backward's P = exp2(c s - lse2) then needs no conversion.
 #include "attn_common.hpp"
+#include "attn_fwd4.hpp"
 
 #include <cstdlib>
 
@@ -1009,6 +1010,38 @@ void launch_fwd(const FwdP& p, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL(attn_fwd16_split_k<D>, dim3(1, grid.y, grid.z), dim3(256), 0, s, p, (const long*)nullptr,
                        0L, 0L, 0L);
     return;
+  }
+  // D 64, bounded softmax, frame mask without documents: the one-wave-per-SIMD forward (attn_fwd4.hip;
+  // OWLK_FWD4=0 keeps attn_fwd16_k, read per call so tests can compare the two)
+  if constexpr (D == 64) {
+    const char* e4 = getenv("OWLK_FWD4");
+    // long sweeps only (global or >= 4096-token windows): at window 16 (1,024 keys) the 512-query
+    // workgroups leave the chip a quarter as many blocks and the run's prologue / drain dominate
+    // (0.73 -> 1.13 ms, profiles/r6z)
+    const bool long4 = p.m.window <= 0 || (long)p.m.window * p.m.tpf >= 4096;
+    if ((!e4 || atoi(e4) != 0) && f16 && p.bound > 0.f && rs && long4) {
+      Fwd4P p4;
+      p4.q = p.q;
+      p4.k = p.k;
+      p4.v = p.v;
+      p4.o = p.o;
+      p4.lse = p.lse;
+      p4.ldq = p.ldq;
+      p4.ldk = p.ldk;
+      p4.ldv = p.ldv;
+      p4.ldo = p.ldo;
+      p4.sqb = p.sqb;
+      p4.skb = p.skb;
+      p4.svb = p.svb;
+      p4.sob = p.sob;
+      p4.Lq = p.Lq;
+      p4.Lkv = p.Lkv;
+      p4.H = p.H;
+      p4.B = (int)grid.z;
+      p4.scale_log2 = p.scale_log2;
+      p4.m = p.m;
+      if (owlk_fwd4_launch(p4, s) == 0) return;
+    }
   }
   // D 128: the 16x16x32 form with 32 queries per wave (OWLK_FWD16_128=0: the 32x32x16 attn_fwd_k)
   static const int f16_128 = getenv("OWLK_FWD16_128") ? atoi(getenv("OWLK_FWD16_128")) : 1;

@@ -35,7 +35,8 @@ OUT = os.path.join(REPO, "owl-audio-exps_amd", "csrc", "attn_bwd_fused4_step.inc
 # before, the first MFMA of the ring DMA pieces and their spacing
 KNOB = {k: int(os.environ.get("F4_" + k.upper(), v))
         for k, v in (("check", 96), ("dma0", 3), ("dmastep", 4), ("pro", 0), ("dqslots", 4), ("xnodma", 0),
-                     ("xnodqr", 0), ("ringv", 0), ("rvl", 49))}  # x*: timing-only experiments (results wrong)
+                     ("xnodqr", 0), ("ringv", 0), ("rvl", 49), ("flagall", 0), ("xprep", 0), ("xend", 0),
+                     ("xbar", 0), ("xexp", 0), ("pollpos", 0), ("xdmaconst", 0), ("chkpoll", 0))}  # x*: timing-only experiments (results wrong)
 
 TILE_BYTES = 64 * 128
 VLO = 96  # the statement's VGPRs: v[VLO:255]
@@ -229,8 +230,8 @@ def build(kind, local, prof=False, P=0):
         out = []
         st0, dp0 = ST(h, t4, 0), DP(h, t4, 0)
         for i in range(8):  # P = exp2(-(lse2 - c s))
-            out.append(Ins(f"v_exp_f32_e64 v{st0 + i}, -v{st0 + i}", "exp", reads=vr(st0 + i, 1), writes=vr(st0 + i, 1),
-                           cost=8))
+            out.append(Ins(f"v_exp_f32_e64 v{st0 + i}, -v{st0 + i}" if not KNOB["xexp"] else f"v_mov_b32 v{st0 + i}, v{st0 + i}",
+                           "exp", reads=vr(st0 + i, 1), writes=vr(st0 + i, 1), cost=8))
         if masked:
             # query row 32 h + 16 qs + 4 g + r of the tile is allowed for key tile t4 iff lo <= . < hi,
             # with %[mlo{t4}] / %[mhi{t4}] = bound - 4 g (per lane)
@@ -280,7 +281,13 @@ def build(kind, local, prof=False, P=0):
     # operations here, so vmcnt(4) waits for the poll (and the ring's DMA, issued before it)
     def check(ringw=False):
         tmp = LR(0, 0)
-        out = [Ins("s_waitcnt vmcnt(4)", "raw")]
+        # (a poll placed after the dQ stores: nothing younger than it at the check)
+        out = [Ins("s_waitcnt vmcnt(0)" if KNOB["pollpos"] > 32 and kind != "empty" else "s_waitcnt vmcnt(4)", "raw")]
+        if KNOB["chkpoll"] and kind != "empty" and not KNOB["pollpos"]:
+            # wait for the poll alone: the ring's DMA (4 or 5 pieces, flags bit 1) and the dQ stores
+            # after it may still fly (the end of the step waits for them)
+            out = [Ins("s_bitcmp1_b32 %[fl], 1\ns_cbranch_scc0 .Lf4c4%=\ns_waitcnt vmcnt(8)\ns_branch .Lf4c5%=\n"
+                       ".Lf4c4%=:\ns_waitcnt vmcnt(4)\n.Lf4c5%=:", "raw")]
         if ringw:  # the next tile's ring rows, staged in v[112:127] / v96 since rvl, into the other slot
             t = ["s_waitcnt vmcnt(0)", "s_bitcmp1_b32 %[fl], 1", "s_cbranch_scc0 .Lf4rw%="]
             t += [f"ds_write_b128 %[rq], {rng('v', 112 + 4 * i, 4)} offset:{SN + (TILE_BYTES if i >= 2 else 0) + 1024 * (i % 2)}"
@@ -396,7 +403,10 @@ def build(kind, local, prof=False, P=0):
             gap = min(gap, due)
             fill[pos[gap]].append(x)
             k += 1
-    prog = [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_nop 3", "nop")] + ([stamp(0)] if prof else []) + poll + pro
+    if KNOB["pollpos"]:
+        fill[pos[KNOB["pollpos"]]] += poll
+    prog = [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_nop 3", "nop")] + ([stamp(0)] if prof else []) + \
+        ([] if KNOB["pollpos"] else poll) + pro
     for n in range(N):
         prog += fill[n]
         prog.append(stream[n][0])
@@ -406,8 +416,9 @@ def build(kind, local, prof=False, P=0):
     return prog
 
 
-def finalize(prog):
-    """Insert lgkmcnt waits and hazard nops; returns the instruction texts and statistics."""
+def finalize(prog, allow_pending=False):
+    """Insert lgkmcnt waits and hazard nops; returns the instruction texts and statistics.  allow_pending:
+    LDS loads may still fly at the end (the caller drains them with lgkmcnt(0) before their use)."""
     out = []
     # LDS bookkeeping
     issued = 0          # LDS ops issued so far
@@ -504,7 +515,7 @@ def finalize(prog):
     # end: the last MFMAs' results / operands are the compiler's again after the statement
     out.append("s_nop 7")
     out.append("s_nop 3")
-    assert not pending, "LDS loads never waited for"
+    assert allow_pending or not pending, "LDS loads never waited for"
     return out, dict(nops=nops, waits=waits, instrs=len(out))
 
 
@@ -575,19 +586,27 @@ def emit_run(local):
     for P in (0, 1):
         t += [f".Lf4L{P}%=:", "s_bitcmp1_b32 %[fl], 3", f"s_cbranch_scc0 .Lf4z{P}%=",
               "s_cmp_eq_u32 %[lout], 0", "s_cbranch_scc1 .Lf4x%=",
-              "s_waitcnt vmcnt(0)",  # the landing zone's loads
+              "s_nop 0" if KNOB["xprep"] else ("s_waitcnt vmcnt(1)" if KNOB["flagall"] else "s_waitcnt vmcnt(0)"),
               f"s_branch .Lf4pd{P}%=", f".Lf4z{P}%=:"]
         t += [f"v_mov_b32 v{112 + i}, 0" for i in range(4)]
         t += [f"ds_write_b128 %[qa], v[112:115] offset:{1024 * e}" for e in range(4)]
         t += [f".Lf4pd{P}%=:"] + bodies[P]
-        t += ["s_cmp_eq_u32 %[lout], 0", f"s_cbranch_scc1 .Lf4v{P}%=", "s_waitcnt vmcnt(4)", f"s_branch .Lf4w{P}%=",
-              f".Lf4v{P}%=:", "s_waitcnt vmcnt(0)", f".Lf4w{P}%=:", "s_waitcnt lgkmcnt(0)", "s_barrier",
+        if KNOB["xend"]:
+            t += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        else:
+            t += ["s_cmp_eq_u32 %[lout], 0", f"s_cbranch_scc1 .Lf4v{P}%=", "s_waitcnt vmcnt(4)", f"s_branch .Lf4w{P}%=",
+                  f".Lf4v{P}%=:", "s_waitcnt vmcnt(0)", f".Lf4w{P}%=:", "s_waitcnt lgkmcnt(0)", "s_barrier"]
+        if KNOB["xbar"]:
+            t[-1] = "s_nop 0"
+        t += [
               # lane 0 of wave 0 raises the flag of tile t + 1 (every wave's dQ stores are done)
-              "s_cmp_eq_u32 %[wid], 0", f"s_cbranch_scc0 .Lf4f{P}%=", "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
+              ] + (["s_cmp_eq_u32 %[wid], 0", f"s_cbranch_scc0 .Lf4f{P}%="] if not KNOB["flagall"] else []) + [
+              "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
               "global_store_dword %[zero], %[fval], %[fb] offset:64 sc1", "s_mov_b64 exec, s[78:79]", f".Lf4f{P}%=:",
+              ] + ([] if KNOB["xdmaconst"] else [
               "s_sub_u32 s64, s64, %[qstep]", "s_subb_u32 s65, s65, 0",
               "s_sub_u32 s66, s66, %[ostep]", "s_subb_u32 s67, s67, 0",
-              "s_sub_u32 s68, s68, 256", "s_subb_u32 s69, s69, 0",
+              "s_sub_u32 s68, s68, 256", "s_subb_u32 s69, s69, 0"]) + [
               "s_sub_u32 s70, s70, 64", "s_subb_u32 s71, s71, 0",
               "s_sub_u32 s72, s72, 0x4000", "s_subb_u32 s73, s73, 0",
               "s_sub_u32 s74, s74, 0x4000",
