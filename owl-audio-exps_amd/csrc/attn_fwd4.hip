@@ -65,15 +65,24 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
   // tiles wholly inside the tensor (the ragged last one is DMA'd with clamped rows, by this code)
   const int nwhole = (int)((p.Lkv - kv_begin) / KT4) < ntiles ? (int)((p.Lkv - kv_begin) / KT4) : ntiles;
 
-  // q' = bf16(c q) fragments (B of S^T: lane (c, g) holds d 32 kd + 8 g .. of query 16 t4 + c), O^T = 0
+#ifndef FWD4_FORM
+#define FWD4_FORM 16
+#endif
+  // query tiles per wave: 8 of 16 (16x16x32 form) or 4 of 32 (32x32x16 form)
+  constexpr int QTN = FWD4_FORM == 32 ? 4 : 8, QTS = FWD4_FORM == 32 ? 32 : 16;
+  const int qlane = FWD4_FORM == 32 ? (lane & 31) : c;  // this lane's query within a query tile
+  const int kh = FWD4_FORM == 32 ? (lane >> 5) : g;     // its key-row group (4 kh + r / acc_row)
+  // q' = bf16(c q) fragments, the B operand of S^T (16x16x32: d 32 kd + 8 g of query 16 t4 + c;
+  // 32x32x16: d 16 ks + 8 h of query 32 qt + (lane & 31)); O^T = 0
   {
-    unsigned qv[8][2][4];
+    constexpr int NK = FWD4_FORM == 32 ? 4 : 2, KW = FWD4_FORM == 32 ? 16 : 32;
+    unsigned qv[QTN][NK][4];
 #pragma unroll
-    for (int t4 = 0; t4 < 8; ++t4) {
-      const long q = r0 + 16 * t4 + c;
+    for (int t4 = 0; t4 < QTN; ++t4) {
+      const long q = r0 + QTS * t4 + qlane;
 #pragma unroll
-      for (int kd = 0; kd < 2; ++kd) {
-        bf16x8 x = q < p.Lq ? *(const bf16x8*)(Q + q * p.ldq + 32 * kd + 8 * g) : bf16x8{};
+      for (int kd = 0; kd < NK; ++kd) {
+        bf16x8 x = q < p.Lq ? *(const bf16x8*)(Q + q * p.ldq + KW * kd + 8 * kh) : bf16x8{};
         float f[8];
         unpack8(x, f);
 #pragma unroll
@@ -83,13 +92,19 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
         for (int e = 0; e < 4; ++e) qv[t4][kd][e] = u[e];
       }
     }
+#if FWD4_FORM == 32
+    // the row-sum selector (A of the 16x16x32 row-sum MFMA): row (lane & 15) < 8 takes k-groups 0 and 2
+    // (lanes of query n), rows >= 8 k-groups 1 and 3 (query n + 16)
+    fwd4_agpr_init(qv, (((lane & 15) < 8) == (((lane >> 4) & 1) == 0)) ? 0x3F803F80u : 0u);
+#else
     fwd4_agpr_init(qv, 0x3F803F80u);  // ones: bf16 1.0 pairs
+#endif
   }
   // each query's allowed keys [klo, khi) (causal, window; ragged rows and queries past Lq: none)
-  int klo[8], khi[8];
+  int klo[QTN], khi[QTN];
 #pragma unroll
-  for (int t4 = 0; t4 < 8; ++t4) {
-    const long q = r0 + 16 * t4 + c;
+  for (int t4 = 0; t4 < QTN; ++t4) {
+    const long q = r0 + QTS * t4 + qlane;
     const int fq = frame_of(m, q);
     const int tpf = (int)m.tpf;
     int lo = 0, hi = (int)p.Lkv;
@@ -115,6 +130,21 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
   // per-lane operands
   const unsigned L0 = lds_u32(smem);
   W4Lane f;
+#if FWD4_FORM == 32
+  // K rows (lane & 31), d chunk 2 ks + h (frag_row<SW_ROW>); V^T frag_tr<SW_TR> of d tile cb
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int r = lane & 31;
+    f.kr[ks] = L0 + (unsigned)(r * 128 + (((2 * ks + (lane >> 5)) ^ swz_row(r)) << 4));
+  }
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int h = lane >> 5, qq = (lane & 15) >> 2, pp = lane & 3, ra = 4 * h + qq;
+    const int ch = 4 * cb + 2 * (g & 1) + (pp >> 1);
+    f.vt[cb] = L0 + (unsigned)(ra * 128 + ((ch ^ swz_tr(ra)) << 4) + 8 * (pp & 1));
+  }
+  constexpr int SWV = SW_TR;
+#else
   f.kr[0] = L0 + (unsigned)(c * 128 + (((0 + g) ^ swz_row(c)) << 4));
   f.kr[1] = L0 + (unsigned)(c * 128 + (((4 + g) ^ swz_row(c)) << 4));
 #pragma unroll
@@ -122,7 +152,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
     const int x = 4 * g + (c >> 2), ch = 2 * ds + ((c & 3) >> 1);
     f.vt[ds] = L0 + (unsigned)(x * 128 + ((ch ^ swz_dual(x)) << 4) + 8 * (c & 1));
   }
-  const GldsOff gk = glds_offsets<SW_ROW>(p.ldk, w, lane), gv = glds_offsets<SW_DUAL>(p.ldv, w, lane);
+  constexpr int SWV = SW_DUAL;
+#endif
+  const GldsOff gk = glds_offsets<SW_ROW>(p.ldk, w, lane), gv = glds_offsets<SWV>(p.ldv, w, lane);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     f.ko[h] = gk.o[h];
@@ -141,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
       tile_glds_fast(buf + 8192, V + c0 * p.ldv, gv, w);
     } else {
       tile_glds<SW_ROW>(buf, K, p.ldk, c0, p.Lkv, w, lane);
-      tile_glds<SW_DUAL>(buf + 8192, V, p.ldv, c0, p.Lkv, w, lane);
+      tile_glds<SWV>(buf + 8192, V, p.ldv, c0, p.Lkv, w, lane);
     }
   };
   if (ntiles > 0) issue(0);
@@ -190,9 +222,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
       fwd4_tile<false>(t % NSLOT4, f, sc, fl);
     } else if (kind == TILE_PARTIAL) {
 #pragma unroll
-      for (int t4 = 0; t4 < 8; ++t4) {
-        f.mlo[t4] = klo[t4] - (int)c0 - 4 * g;
-        f.mhi[t4] = khi[t4] - (int)c0 - 4 * g;
+      for (int t4 = 0; t4 < QTN; ++t4) {
+        f.mlo[t4] = klo[t4] - (int)c0 - 4 * kh;
+        f.mhi[t4] = khi[t4] - (int)c0 - 4 * kh;
       }
       fwd4_tile<true>(t % NSLOT4, f, sc, fl);
     }
@@ -204,6 +236,29 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
   // ---- epilogue: O = O^T / rowsum through this wave's 16 KiB of LDS (whole 128-B rows, chunk x of row
   // r at x ^ (r & 7)), lse = log2(rowsum)
   char* stg = smem + w * 16384;
+#if FWD4_FORM == 32
+  static_for4<4>([&](auto tc) {
+    constexpr int qt = decltype(tc)::value;
+    float o[36];
+    fwd4_acc_read<qt>(o);
+    // the row-sum tile: lane (n, g) holds query n (g < 2) or n + 16 (g >= 2)
+    const int q31 = lane & 31, h = lane >> 5;
+    const float l = __shfl(o[32], q31 < 16 ? q31 : q31 + 16, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int r = 32 * qt + q31;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        bf16x4 v4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v4[e] = (bf16)(o[16 * cb + 4 * jj + e] * inv);
+        *(bf16x4*)(stg + r * 128 + (((4 * cb + jj) ^ (r & 7)) << 4) + 8 * h) = v4;
+      }
+    const long q = r0 + r;
+    if (q < p.Lq && h == 0) p.lse[(b * p.H + head) * p.Lq + q] = l > 0.f ? __log2f(l) : -INFINITY;
+  });
+#else
   static_for4<8>([&](auto tc) {
     constexpr int t4 = decltype(tc)::value;
     float o[17];
@@ -221,6 +276,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd4_k(Fwd4P p) {
     const long q = r0 + r;
     if (q < p.Lq && g == 0) p.lse[(b * p.H + head) * p.Lq + q] = l > 0.f ? __log2f(l) : -INFINITY;
   });
+#endif
   wave_lds_handoff();
 #pragma unroll
   for (int it = 0; it < 16; ++it) {

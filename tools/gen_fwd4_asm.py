@@ -49,6 +49,9 @@ NQ = 8                 # 16-query tiles per wave
 SLOT = 16384           # ring slot: K 64 x 128 B | V 64 x 128 B
 VOFF = 8192
 NSLOT = 3
+# timing-only experiment builds (results wrong): W4F_XNODMA=1 no ring DMA, W4F_XEXP=1 v_exp -> v_mov
+XNODMA = int(os.environ.get("W4F_XNODMA", "0"))
+XEXP = int(os.environ.get("W4F_XEXP", "0"))
 
 
 def QF(t4, kd):
@@ -133,7 +136,7 @@ def e_valu(b, t4s, tag, masked=False, kc=0):
         for kk in range(2):
             s0 = ST(b, kk, t4)
             for r in range(4):
-                out.append(Ins(f"v_exp_f32_e32 v{s0 + r}, v{s0 + r}", "exp", reads=vr(s0 + r, 1), writes=vr(s0 + r, 1),
+                out.append(Ins(f"v_exp_f32_e32 v{s0 + r}, v{s0 + r}" if not XEXP else f"v_mov_b32 v{s0 + r}, v{s0 + r}", "exp", reads=vr(s0 + r, 1), writes=vr(s0 + r, 1),
                                cost=8, meta=("E", s0 + r, kk, t4, tag)))
             if masked:
                 for r in range(4):
@@ -183,6 +186,9 @@ def dma(slot, counted=False):
     for i in range(4):
         src, off = ("kb", f"ko{i % 2}") if i < 2 else ("vb", f"vo{i % 2}")
         dst = slot * SLOT + (VOFF if i >= 2 else 0) + 1024 * (i % 2)
+        if XNODMA:
+            out.append(Ins("s_nop 0", "raw"))
+            continue
         t = ["s_cmp_gt_i32 s69, 0" if counted else "s_bitcmp1_b32 %[fl], 0", f"s_cbranch_scc0 .Lw4d{i}%=",
              f"s_add_u32 m0, %[m0k], {dst}", "s_nop 0", f"global_load_lds_dwordx4 %[{off}], %[{src}]", f".Lw4d{i}%=:"]
         out.append(Ins("\n".join(t), "raw"))
