@@ -197,6 +197,10 @@ template <int N, typename A, typename B>
 DEV void lgkm2(A& a, B& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
+template <int N, typename A, typename B, typename C>
+DEV void lgkm3(A& a, B& b, C& c) {
+  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N) : "memory");
+}
 template <int N, typename A, typename B, typename C, typename D>
 DEV void lgkm4(A& a, B& b, C& c, D& d) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");

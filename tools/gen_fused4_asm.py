@@ -218,8 +218,10 @@ def build(kind, local, prof=False, P=0):
     def rd_dq(k2):  # K^T (image rows 16 k2 ..) and dS^T fragments of dQ k-step k2 (frag_tr of attn_bwd_fused_k)
         r = DQR(k2 % NS)
         # (the dS image of tile t + 1: the other one)
-        return [Ins(f"ds_read_b64_tr_b16 {rng('a', r + 2 * i, 2)}, %[{nm}] offset:{2048 * k2 + (i // 2) * (1 - P) * DS_BYTES}",
-                    "ldsr", writes=ar(r + 2 * i, 2), lds=True) for i, nm in enumerate(("ka", "kb", "sa", "sb"))]
+        # K^T fragment: one ds_read_b128 of the lane-linear fragment image (attn_bwd_fused4.hip)
+        return [Ins(f"ds_read_b128 {rng('a', r, 4)}, %[kf] offset:{1024 * k2}", "ldsr", writes=ar(r, 4), lds=True)] + \
+            [Ins(f"ds_read_b64_tr_b16 {rng('a', r + 2 * i, 2)}, %[{nm}] offset:{2048 * k2 + (1 - P) * DS_BYTES}",
+                 "ldsr", writes=ar(r + 2 * i, 2), lds=True) for i, nm in ((2, "sa"), (3, "sb"))]
 
     def rd_qacc():  # the dQ sum so far (predecessor's, zeros or NaN), lane-linear in the landing zone
         return [Ins(f"ds_read_b128 {rng('v', QA + 4 * e, 4)}, %[qa] offset:{1024 * e}", "ldsr", writes=vr(QA + 4 * e, 4),
@@ -519,7 +521,7 @@ def finalize(prog, allow_pending=False):
     return out, dict(nops=nops, waits=waits, instrs=len(out))
 
 
-VOPS = ["ar0", "ar1", "al", "tr0", "tr1", "tr2", "tr3", "ds0", "ds1", "ds2", "ds3", "qa", "ka", "kb", "sa", "sb", "soffa",
+VOPS = ["ar0", "ar1", "al", "tr0", "tr1", "tr2", "tr3", "ds0", "ds1", "ds2", "ds3", "qa", "kf", "sa", "sb", "soffa",
         "soffr", "flagv", "qo0", "qo1", "oo0", "oo1", "lo", "zero", "rq", "rl"]
 SOPS = [("rsrc", "__amdgpu_buffer_rsrc_t"), ("fl", "int"), ("nscale", "float"), ("want", "int"), ("soffs", "int"),
         ("sumbase", "const void*"), ("m0a", "unsigned"), ("m0f", "unsigned"), ("m0q", "unsigned"), ("m0l", "unsigned"),
@@ -699,7 +701,7 @@ def main():
            "// immediate), the landing zone, the K^T and dS^T reads of dQ; dQ store offsets (fp32 sum / bf16 rows),\n"
            "// the polled flag; the ring DMA's source offsets (Q / dO rows h, lse2 or delta); a zero\n"
            "struct F4Lane {\n"
-           "  unsigned ar0, ar1, al, tr[4], dsa[4], qa, ka, kb, sa, sb, soffa, soffr, flagv, qo[2], oo[2], lo, zero, rq, rl;\n"
+           "  unsigned ar0, ar1, al, tr[4], dsa[4], qa, kf, sa, sb, soffa, soffr, flagv, qo[2], oo[2], lo, zero, rq, rl;\n"
            "  int mlo[4], mhi[4];  // PARTIAL tiles: allowed query rows per key tile, relative to the tile, - 4 g\n"
            "};\n"
            "// wave-uniform operands (SGPR): the dQ store target (accumulator / dq rows / none) with flags bit 0 =\n"
