@@ -1,0 +1,136 @@
+"""The ping-pong GEMM's paired-rounding epilogues (gemm.hip epi_apply2, OWLK_GEMM_EPI2=1), bit for bit.
+
+Shapes of >= 192 256^2 tiles take gemm_pp_kernel (M 8,232 is ragged: its last tile row is partial).
+The fp32 accumulator comes from the same kernel with an fp32 STORE output (same main loop, same tile
+order, alpha 1: v = acc exactly), and each epilogue's rounding chain is replayed on it in torch:
+bias rounded to bf16, RNE conversions, the products in the order the kernel forms them.  alpha / beta
+of the fused multiply-adds are powers of two (the FMA then rounds like the separate operations), so
+STORE (bias, beta), AXPBY, SCALE2 and GATE_RESID must match exactly; SILU's aux output exactly and its
+silu (hardware exp / rcp) within one bf16 ulp; DSILU within one ulp of the fp32 chain.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def K():
+    from owl_wms import kernels
+    return kernels
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _needs_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from owl_wms._lib import lib
+    lib()
+
+
+M, N, KD = 8192 + 40, 2048, 512
+
+
+def data(seed):
+    g = torch.Generator().manual_seed(seed)
+    A = (torch.randn(M, KD, generator=g) * 0.5).bfloat16().to(DEV)
+    B = (torch.randn(N, KD, generator=g) * 0.05).bfloat16().to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.3).float().to(DEV)
+    x = torch.randn(M, N, generator=g).bfloat16().to(DEV)
+    return A, B, bias, x
+
+
+def acc_of(k, A, B):
+    return k.gemm(A, B, out_f32=True)
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def ulps(a, b):
+    """bf16 ulp distance on the monotonic integer line (-0 == +0)"""
+    def key(t):
+        i = t.contiguous().view(torch.int16).int()
+        return torch.where(i >= 0, i, -32768 - i)
+    return (key(a) - key(b)).abs()
+
+
+def test_store_bias_beta_exact():
+    k = K()
+    A, B, bias, x = data(1)
+    acc = acc_of(k, A, B)
+    c = x.clone()
+    k.gemm(A, B, out=c, epi=k.EPI_STORE, alpha=1.0, beta=0.5, bias=bias)
+    v = acc + bf(bias).float()
+    v = v + 0.5 * x.float()
+    assert torch.equal(c, bf(v))
+
+
+def test_axpby_exact():
+    k = K()
+    A, B, bias, x = data(2)
+    acc = acc_of(k, A, B)
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    k.gemm(A, B, out=c, epi=k.EPI_AXPBY, alpha=0.75, beta=-1.25, aux=x)
+    r = bf(acc).float()
+    s1 = bf(0.75 * r).float()
+    s2 = bf(-1.25 * x.float()).float()
+    assert torch.equal(c, bf(s1 + s2))
+
+
+def test_scale2_exact():
+    k = K()
+    A, B, bias, x = data(3)
+    acc = acc_of(k, A, B)
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aux = torch.empty_like(c)
+    k.gemm(A, B, out=c, epi=k.EPI_SCALE2, alpha=0.3, aux=aux)
+    y = bf(acc)
+    assert torch.equal(c, y)
+    assert torch.equal(aux, bf(0.3 * y.float()))
+
+
+@pytest.mark.parametrize("tpf", [1, 64])
+def test_gate_resid_exact(tpf):
+    k = K()
+    A, B, bias, x = data(4)
+    g = torch.Generator().manual_seed(40)
+    F = (M + tpf - 1) // tpf
+    gate = torch.randn(F, N, generator=g).bfloat16().to(DEV)
+    acc = acc_of(k, A, B)
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aux = torch.empty_like(c)
+    k.gemm(A, B, out=c, epi=k.EPI_GATE_RESID, bias=bias, aux=aux, gate=gate, tpf=tpf, resid=x)
+    y = bf(acc + bf(bias).float())
+    gm = gate.float()[torch.arange(M, device=DEV) // tpf]
+    t = bf(gm * y.float())
+    assert torch.equal(aux, y)
+    assert torch.equal(c, bf(x.float() + t.float()))
+
+
+def test_silu_aux_exact_out_one_ulp():
+    k = K()
+    A, B, bias, x = data(5)
+    acc = acc_of(k, A, B)
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aux = torch.empty_like(c)
+    k.gemm(A, B, out=c, epi=k.EPI_SILU, bias=bias, aux=aux)
+    y = bf(acc + bf(bias).float())
+    assert torch.equal(aux, y)
+    ref = bf(torch.nn.functional.silu(y.float()))
+    assert ulps(c, ref).max().item() <= 1
+
+
+def test_dsilu_one_ulp():
+    k = K()
+    A, B, bias, x = data(6)
+    acc = acc_of(k, A, B)
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    act = torch.empty_like(c)
+    k.gemm(A, B, out=c, epi=k.EPI_DSILU, aux=x, resid=act)
+    xf = x.float()
+    sg = torch.sigmoid(xf)
+    ref = bf(bf(acc).float() * sg * (1.0 + xf * (1.0 - sg)))
+    assert ulps(c, ref).max().item() <= 1
+    assert ulps(act, bf(torch.nn.functional.silu(xf))).max().item() <= 1
