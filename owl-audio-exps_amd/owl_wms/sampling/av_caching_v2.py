@@ -38,6 +38,7 @@ class AVCachingSamplerV2:
         self.max_window = max_window
         self.custom_schedule = custom_schedule
         self._pool = None  # graph memory pool shared by the per-frame captures (compile_on_decode)
+        self._graph_prev = None  # (graph, event) of the previous frame (compile_on_decode, host-position path)
         self._step_graph = None
         # keep the cache position on the device so one captured Euler step serves every frame
         # (False: the host-position path, one capture per frame with the cache length baked in)
@@ -91,7 +92,14 @@ class AVCachingSamplerV2:
             sdt.copy_(dt[t_idx])
             g.replay()
         out = sx.clone(), st.clone()
-        _release_graph(g)
+        # keep this frame's graph until the next frame's replays are queued, then release the previous
+        # one behind its own event (its replays ran long before): no full-stream sync per frame
+        ev = torch.cuda.Event()
+        ev.record()
+        prev, self._graph_prev = self._graph_prev, (g, ev)
+        if prev is not None:
+            prev[1].synchronize()
+            prev[0].reset()
         return out
 
     def _euler_replay(self, model, kv_cache, x, t, mouse, btn, null_mouse, null_btn, dt):
@@ -164,6 +172,7 @@ class AVCachingSamplerV2:
 
         num_frames = min(self.num_frames, mouse.size(1) - init_len)
         self._step_graph = None
+        self._graph_prev = None
         # the cache position on the device (one captured step for every frame); the same kernels run
         # in eager mode too, so eager and graphed decode stay bit-identical
         cfgm = model.config
@@ -201,4 +210,7 @@ class AVCachingSamplerV2:
             if self._step_graph is not None:
                 _release_graph(self._step_graph[0])
             self._step_graph = None
+            if self._graph_prev is not None:
+                _release_graph(self._graph_prev[0])
+            self._graph_prev = None
         return torch.cat(latents, dim=1)

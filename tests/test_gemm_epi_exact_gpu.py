@@ -134,3 +134,37 @@ def test_dsilu_one_ulp():
     ref = bf(bf(acc).float() * sg * (1.0 + xf * (1.0 - sg)))
     assert ulps(c, ref).max().item() <= 1
     assert ulps(act, bf(torch.nn.functional.silu(xf))).max().item() <= 1
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_split256_wgrad_plan_deterministic(beta):
+    """The 256^2 split-K plan for the cond-gradient shape (K 9,216 >= 8,192, fewer than 128 256^2 tiles,
+    fp32 out with the workspace, beta 0 and 1): deterministic bit for bit, and == fp32 torch."""
+    k = K()
+    g = torch.Generator().manual_seed(7)
+    dy = torch.randn(9216, 1536, generator=g).bfloat16().to(DEV)
+    x = torch.randn(9216, 1536, generator=g).bfloat16().to(DEV)
+    c0 = torch.randn(1536, 1536, generator=g).float().to(DEV)
+    outs = []
+    for _ in range(2):
+        out = c0.clone()
+        k.gemm(dy, x, a_trans=True, b_trans=True, out=out, out_f32=True, beta=beta)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    ref = dy.float().t() @ x.float() + (c0 if beta else 0.0)
+    err = ((outs[0] - ref).norm() / ref.norm()).item()
+    assert err < 1e-5, err
+
+
+def test_modulation_shape_pingpong_bias():
+    """[1,536 x 9,216 x 1,536] bf16 + bias: 216 256^2 tiles, above the ping-pong minimum of 192."""
+    k = K()
+    g = torch.Generator().manual_seed(8)
+    A = torch.randn(1536, 1536, generator=g).bfloat16().to(DEV)
+    B = (torch.randn(9216, 1536, generator=g) * 0.05).bfloat16().to(DEV)
+    bias = torch.randn(9216, generator=g).float().to(DEV)
+    c = k.gemm(A, B, bias=bias)
+    acc = k.gemm(A, B, out_f32=True)
+    assert torch.equal(c, bf(acc + bf(bias).float()))
+    ref = A.float() @ B.float().t() + bf(bias).float()
+    assert ((c.float() - ref).norm() / ref.norm()).item() < 1e-2
