@@ -1440,7 +1440,7 @@ struct SplitPlan {
 // frames: frame-strided operand rows (owlk_gemm_frames) -- only the 256^2 kernel reads them, so
 // neither the decode plan nor the skinny split-K plan may be taken
 static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
-                            float beta, bool frames = false) {
+                            float beta, bool frames = false, bool allow_opt = true) {
   SplitPlan pl{SPLIT_NONE, 1, K, false};
   static const int use_decode = getenv("OWLK_GEMM_DECODE") ? atoi(getenv("OWLK_GEMM_DECODE")) : 1;
   if (use_decode && !frames && M <= 128 && batch == 1 && !a_trans && !b_trans && !c_f32 && N % DEC_T == 0 && K % 32 == 0 &&
@@ -1470,8 +1470,8 @@ static SplitPlan split_plan(long M, long N, long K, long batch, int a_trans, int
         return pl;
       }
     }
-    if (c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 && K < 16384 &&
-        tiles256 < 128) {
+    if (allow_opt && c_f32 && epi == EPI_STORE && batch == 1 && (beta == 0.f || beta == 1.f) && K >= 8192 &&
+        K < 16384 && tiles256 < 128) {
       // few tiles, mid K (the per-frame cond gradient [1,536 x 1,536 x 9,216]: 108 -> 62 us): one round
       // of 256^2 splits of >= 1,024 instead of the 128^2 kernel's two, with a workspace only (without:
       // the unsplit plan, deterministic, rather than fp32 atomics).  At K = 1,536 (the modulation
@@ -1552,9 +1552,18 @@ static int gemm_dispatch(GemmP& p, long M, long N, long K, long batch,
   const bool frames = p.a_fs || p.b_fs || p.c_fs;
   SplitPlan pl = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta, frames);
   const long pws = split_ws_bytes(pl, M, N, batch);
-  const bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
+  bool have_ws = ws && (uintptr_t)ws % 16 == 0 && pws > 0 && ws_bytes >= pws;
   static const int atomic_splitk = getenv("OWLK_GEMM_ATOMIC") ? atoi(getenv("OWLK_GEMM_ATOMIC")) : 0;
-  if (pl.opt && (!have_ws || atomic_splitk)) pl = SplitPlan{SPLIT_NONE, 1, K, false};
+  if (pl.opt && (!have_ws || atomic_splitk)) {
+    // the opt plan needs its workspace: with fp32 atomics asked for (OWLK_GEMM_ATOMIC), or a
+    // workspace that covers the 128^2 plan, take the plan the shape had before it; else unsplit
+    // (deterministic) rather than atomics nobody asked for
+    const SplitPlan p128 = split_plan(M, N, K, batch, a_trans, b_trans, c_f32, epi, beta, frames, false);
+    const long w128 = split_ws_bytes(p128, M, N, batch);
+    const bool ws128 = ws && (uintptr_t)ws % 16 == 0 && w128 > 0 && ws_bytes >= w128;
+    pl = (atomic_splitk || ws128) ? p128 : SplitPlan{SPLIT_NONE, 1, K, false};
+    have_ws = ws128;
+  }
   if (pl.kind == SPLIT_DECODE && (pl.splits == 1 || have_ws)) return launch_decode(p, epi, ws, s);
   {
     const long sk = pl.splits;

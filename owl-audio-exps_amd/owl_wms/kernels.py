@@ -455,10 +455,13 @@ def fused_bwd_variant(D, mask):
     # traffic against all three of dit_v4's at once (profiles/r4j_ab.log)
     group = int(os.environ.get("OWLK_BWD_FUSED_GROUP", "1"))
     # OWLK_BWD_FUSED_W4 (variant bit 7): the one-wave-per-SIMD kernel with the hand-placed step
-    # (attn_bwd_fused4.hip) -- "global" (default): layers without a window (its per-item fixed cost
-    # loses on the short sweeps of windowed layers), "1": every layer, "0": none
-    w4env = os.environ.get("OWLK_BWD_FUSED_W4", "global")
-    w4 = 128 if (w4env == "1" or (w4env == "global" and mask.window is None)) else 0
+    # (attn_bwd_fused4.hip) -- "long" (default; "global" is the same): layers without a window or with
+    # windows of >= 8,192 tokens (its per-item fixed cost loses on short sweeps: mmdit_v2-like tpf 65,
+    # 24 heads x 1000 frames: window 256 frames 15.41 -> 14.90 ms, window 64 4.69 -> 4.77, window 16
+    # 1.52 -> 1.88, profiles/r6ah_mmdit_w4.log), "1": every layer, "0": none
+    w4env = os.environ.get("OWLK_BWD_FUSED_W4", "long")
+    long_sweep = mask.window is None or int(mask.window) * int(mask.tpf) >= 8192
+    w4 = 128 if (w4env == "1" or (w4env in ("long", "global") and long_sweep)) else 0
     # FUSED_FAIL_TEST (tests only, set through monkeypatch; variant bit 6): chain 0's block-1 hand-off
     # waits time out, so the error path -- the error word and NaN dQ rows -- is exercised through
     # this entry.  A module attribute, not an environment variable: one left exported would turn

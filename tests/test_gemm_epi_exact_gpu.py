@@ -168,3 +168,26 @@ def test_modulation_shape_pingpong_bias():
     assert torch.equal(c, bf(acc + bf(bias).float()))
     ref = A.float() @ B.float().t() + bf(bias).float()
     assert ((c.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+def test_split256_opt_plan_without_workspace():
+    """The cond-gradient shape through the C ABI with no workspace: the opt split plan needs one, so the
+    GEMM runs unsplit (deterministic: two runs equal) -- or the 128^2 split plan when a workspace for
+    that one is given or atomics are asked for (gemm.hip)."""
+    from owl_wms import _lib
+    Mx, Nx, Kx = 1536, 1536, 9216
+    g = torch.Generator().manual_seed(9)
+    dy = torch.randn(Kx, Mx, generator=g).bfloat16().to(DEV)
+    x = torch.randn(Kx, Nx, generator=g).bfloat16().to(DEV)
+    ref = dy.float().t() @ x.float()
+    for beta in (0.0, 1.0):
+        outs = []
+        for _ in range(2):
+            out = torch.zeros(Mx, Nx, device=DEV) if beta == 0.0 else torch.ones(Mx, Nx, device=DEV)
+            _lib.call("owlk_gemm", Mx, Nx, Kx, 1, _lib.ptr(dy), dy.stride(0), 0, 1, _lib.ptr(x), x.stride(0), 0, 1,
+                      _lib.ptr(out), out.stride(0), 0, 1, 0, 1.0, beta, None, None, 0, 0, None, 0, 0, 1, None, 0, 0,
+                      None, None, 0, _lib.stream())
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1])
+        err = ((outs[0] - (ref + beta)).norm() / (ref + beta).norm()).item()
+        assert err < 1e-5, err
