@@ -460,7 +460,8 @@ def fused_bwd_variant(D, mask):
     # 24 heads x 1000 frames: window 256 frames 15.41 -> 14.90 ms, window 64 4.69 -> 4.77, window 16
     # 1.52 -> 1.88, profiles/r6ah_mmdit_w4.log), "1": every layer, "0": none
     w4env = os.environ.get("OWLK_BWD_FUSED_W4", "long")
-    long_sweep = mask.window is None or int(mask.window) * int(mask.tpf) >= 8192
+    # packed documents stay on the 8-wave kernel (the W4 steady-run statement does not cover them)
+    long_sweep = (mask.window is None or int(mask.window) * int(mask.tpf) >= 8192) and mask.arrays is None
     w4 = 128 if (w4env == "1" or (w4env in ("long", "global") and long_sweep)) else 0
     # FUSED_FAIL_TEST (tests only, set through monkeypatch; variant bit 6): chain 0's block-1 hand-off
     # waits time out, so the error path -- the error word and NaN dQ rows -- is exercised through
