@@ -216,6 +216,12 @@ int owlk_attn_bwd_fused(const void* q, long ldq, long sqb, const void* k, long l
                         long tpf, int window, int causal, const int* kv_lo, const int* q_hi,
                         const int* run_start, const int* doc, long fstride, void* ws, long ws_bytes,
                         int variant, void* stream);
+/* CUs the persistent single-pass backward leaves free for kernels on other streams (the gradient
+ * all-reduce of the synchronising micro-step, utils/grad_reducer.py): its grid becomes (CUs - cus)
+ * workgroups per CU-slot, at least one per XCD.  Process-wide; 0 (default) = every CU.  Replaces
+ * nothing in the reference: DDP's bucketed all-reduce overlaps backward there (rft_trainer.py:95-99),
+ * and on MI355X a persistent grid on every CU would hold a bucket's collective until it ends. */
+int owlk_set_cu_reserve(int cus);
 
 /* ---- Flow-matching noise + patchify (gamerft.py:92-95,107-108,52): x, z [BN, C, P] bf16,
  *   ts_raw [BN] fp32 (bf16-valued randn) -> xt, tgt token-major [BN*P, C]; ts_out = bf16 sigmoid */

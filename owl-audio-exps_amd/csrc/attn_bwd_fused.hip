@@ -37,6 +37,9 @@
 // predecessor that is done or running.
 // Spins are bounded by the real-time clock (error word in the workspace header).
 
+#include <algorithm>
+#include <atomic>
+
 #include "attn_fused_common.hpp"
 
 
@@ -788,19 +791,28 @@ __global__ __launch_bounds__(256) void fused_drain_check_k(FusedP p) {
   }
 }
 
+// CUs left to other streams' kernels (owlk_set_cu_reserve): the persistent grid shrinks by that many
+// CUs' workgroups, so an all-reduce launched beside it finds free CUs instead of waiting for its end
+std::atomic<int> g_cu_reserve{0};
+
 int fused_grid(int dev, bool w4) {
-  static int cached[64][2] = {};
+  static int cached[64][2][2] = {};  // {CUs, workgroups per CU}
   if (dev < 0 || dev >= 64) dev = 0;
-  if (!cached[dev][w4]) {
+  if (!cached[dev][w4][0]) {
     int cus = 0, per = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (w4)
       per = fused4_occupancy();
     else
       (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, attn_bwd_fused_k<false, false>, 512, 0);
-    cached[dev][w4] = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+    cached[dev][w4][1] = per > 0 ? per : 1;
+    cached[dev][w4][0] = cus > 0 ? cus : 256;
   }
-  return cached[dev][w4];
+  const int cus = cached[dev][w4][0], per = cached[dev][w4][1];
+  // workgroups reach the XCDs round-robin: (CUs - k) keeps every XCD's queue drained as long as at
+  // least one workgroup per XCD remains (8 CUs)
+  const int keep = std::max(std::min(cus, 8), cus - g_cu_reserve.load(std::memory_order_relaxed));
+  return keep * per;
 }
 
 // the XCD-local hand-off needs a workgroup on every one of the 8 per-XCD queues' XCDs (an XCC id
@@ -819,6 +831,12 @@ bool all_xcds_present(int dev) {
 }  // namespace
 
 static long fused_tiles(long L) { return (L + FQT - 1) / FQT; }
+
+extern "C" int owlk_set_cu_reserve(int cus) {
+  OWLK_REQUIRE(cus >= 0, "owlk_set_cu_reserve: negative CU count %d", cus);
+  g_cu_reserve.store(cus, std::memory_order_relaxed);
+  return 0;
+}
 
 extern "C" long owlk_attn_bwd_fused_ws_bytes(long B, int H, long L, int head_dim) {
   if (head_dim != 64 || B <= 0 || H <= 0 || L <= 0) return 0;

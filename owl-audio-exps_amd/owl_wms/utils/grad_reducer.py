@@ -11,13 +11,20 @@
   backward of earlier layers continues on the compute stream.  Earlier micro-steps do not
   communicate (equal to the reference's per-micro-step all-reduce up to fp32 summation order).
 * ``finish()`` waits for every launched bucket and averages (ReduceOp.AVG when available).
+* The persistent single-pass attention backward holds every CU for its whole launch, so a bucket
+  issued beside it would wait for its end.  On the synchronising micro-step over RCCL
+  the reducer asks libowlk, from its first bucket launch on, to leave ``reserve_cus`` CUs free
+  (``owlk_set_cu_reserve``; default 32 = four per XCD, env ``OWL_RCCL_RESERVE_CUS``) and restores the
+  full grid in ``finish()``.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 
 class GradReducer:
-    def __init__(self, params, bucket_mb=256, world_size=None, process_group=None):
+    def __init__(self, params, bucket_mb=256, world_size=None, process_group=None, reserve_cus=None):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.ws = world_size if world_size is not None else (dist.get_world_size() if dist.is_initialized() else 1)
@@ -48,6 +55,10 @@ class GradReducer:
         self.sync = False
         nccl = self.ws > 1 and dist.is_initialized() and dist.get_backend(self.pg) == "nccl"
         self.op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM  # RCCL averages in-collective
+        if reserve_cus is None:
+            reserve_cus = int(os.environ.get("OWL_RCCL_RESERVE_CUS", "32"))
+        self.reserve_cus = reserve_cus if nccl else 0  # gloo collectives run on the host
+        self._reserved = False
         self.pending = [0] * len(self.buckets)
         self.works = []
         self.ready = set()
@@ -92,6 +103,8 @@ class GradReducer:
             self._launch(bi)
 
     def _launch(self, bi):
+        if self.reserve_cus > 0 and not self._reserved:  # backward launches from here on leave CUs free
+            self._reserve(self.reserve_cus)
         self.works.append((dist.all_reduce(self.flat[bi], op=self.op, group=self.pg, async_op=True), bi, self.op))
 
     def finish(self):
@@ -107,6 +120,13 @@ class GradReducer:
                 self.flat[bi].div_(self.ws)
         self.works = []
         self.sync = False
+        if self._reserved:
+            self._reserve(0)
+
+    def _reserve(self, cus):
+        from .. import _lib
+        _lib.call("owlk_set_cu_reserve", cus)
+        self._reserved = cus > 0
 
 
 class EMA:

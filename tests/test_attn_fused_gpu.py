@@ -185,6 +185,38 @@ def test_attention_bwd_fused_deterministic(case):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("variant", [1, 129])
+def test_attention_bwd_fused_cu_reserve(variant):
+    """owlk_set_cu_reserve (the gradient all-reduce's room, utils/grad_reducer.py): the persistent grid
+    shrinks to (CUs - k) workgroups per CU-slot, at least one per XCD, so every per-XCD queue is still
+    drained (error word 0) and the ordered hand-off gives the full grid's bits at k = 8, 16 and a k
+    past the CU count (clamped to 8 CUs)."""
+    from owl_wms import _lib
+    k = K()
+    B, H, nf, tpf = 1, 4, 48, 64
+    D, L = 64, nf * tpf
+    q, kk, v, do = _inputs(B, H, L, D, 400)
+    mask = k.FrameMask(tpf, None, True)
+    o, lse = k.attn_fwd(q, kk, v, H, D, mask)
+    delta = _delta(o, do, H, D)
+    runs = []
+    try:
+        for cus in (0, 8, 16, 100000):
+            _lib.call("owlk_set_cu_reserve", cus)
+            g = [torch.full_like(q, float("nan")) for _ in range(3)]
+            ws = k.attn_bwd_fused(q, kk, v, do, lse, delta, H, D, mask, *g, D ** -0.5, variant)
+            torch.cuda.synchronize()
+            assert _hdr(ws)[8].item() == 0, f"reserve {cus}: error word set"
+            runs.append(g)
+    finally:
+        _lib.call("owlk_set_cu_reserve", 0)
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    with pytest.raises(RuntimeError):
+        _lib.call("owlk_set_cu_reserve", -1)
+
+
 @pytest.mark.parametrize("variant", [2, 3, 7, 131])
 @pytest.mark.parametrize("shape", [(1, 24, 1536, 64, True, None), (2, 3, 20, 64, True, None), (1, 1, 300, 1, True, None),
                                    (1, 2, 40, 64, False, None), (1, 8, 96, 65, True, None),

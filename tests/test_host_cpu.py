@@ -4,6 +4,7 @@ import ctypes
 import json
 import os
 import re
+import socket
 
 import pytest
 import torch
@@ -190,6 +191,31 @@ def test_frame_arrays_bruteforce(window):
                 assert rs[f] == 0 or doc[b, rs[f] - 1] != doc[b, f]
 
 
+def test_grad_reducer_cu_reserve_brackets_the_sync_micro_step(monkeypatch):
+    """The CU reserve for RCCL (owlk_set_cu_reserve) is asked for at the first bucket launch of the
+    synchronising micro-step and dropped in finish(); never on gloo, never on earlier micro-steps."""
+    import owl_wms.utils.grad_reducer as gr
+
+    class _Work:
+        def wait(self):
+            pass
+
+    monkeypatch.setattr(gr.dist, "all_reduce", lambda *a, **k: _Work())
+    model = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.Linear(8, 2))
+    red = gr.GradReducer(model.parameters(), bucket_mb=0.0001, world_size=2)
+    assert red.reserve_cus == 0  # no RCCL process group here
+    red.reserve_cus = 32
+    calls = []
+    monkeypatch.setattr(red, "_reserve", lambda cus: (calls.append(cus), setattr(red, "_reserved", cus > 0)))
+    for micro in range(3):
+        red.begin(sync=micro == 2)
+        model(torch.randn(3, 4)).sum().backward()
+        if micro < 2:
+            assert calls == []
+        red.finish()
+    assert len(red.buckets) > 1 and calls == [32, 0]
+
+
 # ------------------------------------------------------------------ world_size 2 on gloo
 # one numel (96) in three shapes: the group mixes transposed (r > c) and plain NS layouts, and 5
 # params over 2 ranks leave the last chunk short
@@ -253,7 +279,9 @@ def test_reducer_and_muon_world_size(ws):
     """ws 8 = the bench's largest node: 5 Muon matrices over 8 ranks leave ranks that own none."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() * 7 + ws) % 1000
+    with socket.socket() as sk:  # a free port (a fixed one can still be held by an earlier run)
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
     procs = [ctx.Process(target=_worker, args=(r, ws, port, q)) for r in range(ws)]
     for p in procs:
         p.start()

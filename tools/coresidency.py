@@ -1,14 +1,16 @@
 """Can a collective run beside the single-pass attention backward?
 
-The global-layer attn_bwd_fused launch is a persistent grid of one 512-thread workgroup per CU with
-147.5 KiB of LDS and 256 VGPRs per wave (two waves per SIMD: the whole register file).  RCCL's
-all-reduce kernels run on their own stream (utils/grad_reducer.py).  This probe launches, on a second
-stream, a kernel with an RCCL-like footprint (tools/coresid_kernel.hip: 32 persistent workgroups of 256
-threads, 8 KiB LDS, streaming a 256 MiB gradient bucket) while the fused kernel runs, and the other way
-round, and reads the 100 MHz real-time clock stamped by every workgroup and around the fused launch.
+The global-layer attn_bwd_fused launch is a persistent grid of one workgroup per CU (round 6: the
+one-wave-per-SIMD kernel, 4 waves x 512 registers, 147.5 KiB of LDS: nothing else fits beside it).
+RCCL's all-reduce kernels run on their own stream (utils/grad_reducer.py).  This probe launches, on a
+second stream, a kernel with an RCCL-like footprint (tools/coresid_kernel.hip: 32 persistent
+workgroups of 256 threads, 8 KiB LDS, streaming a 256 MiB gradient bucket) while the fused kernel
+runs, and the other way round, and reads the 100 MHz real-time clock stamped by every workgroup and
+around the fused launch -- once per CU reserve in RESERVE (owlk_set_cu_reserve: the grid shrinks to
+CUs - k).
 
-    python tools/coresidency.py   (build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC
-                                   tools/coresid_kernel.hip -o tools/_coresid.so)
+    RESERVE=0,8,16 python tools/coresidency.py
+    (build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC tools/coresid_kernel.hip -o tools/_coresid.so)
 """
 import ctypes
 import json
@@ -66,6 +68,17 @@ def main():
     fused()
     copy(main_s)
     torch.cuda.synchronize()
+    out = {}
+    for cus in [int(x) for x in os.environ.get("RESERVE", "0").split(",")]:
+        _lib.call("owlk_set_cu_reserve", cus)  # the grid the all-reduce micro-step launches (grad_reducer.py)
+        out[f"reserve_{cus}"] = probe(fused, copy, now, marks, stamps, NWG, side, main_s)
+    _lib.call("owlk_set_cu_reserve", 0)
+    print(json.dumps(out, indent=1))
+
+
+def probe(fused, copy, now, marks, stamps, NWG, side, main_s):
+    fused()
+    torch.cuda.synchronize()
     res = {}
     # alone
     now(0, main_s); fused(); now(1, main_s); torch.cuda.synchronize()
@@ -90,6 +103,8 @@ def main():
             "copy_first_wg_start_after_fused_start_ms": (first - m[0]) / 1e5,
             "copy_last_wg_end_after_fused_end_ms": (last - m[1]) / 1e5,
             "copy_wgs_started_before_fused_end": sum(1 for a, _ in st if a < m[1]),
+            "copy_wgs_ended_before_fused_end": sum(1 for _, b in st if b < m[1]),
+            "copy_wg_end_ms_after_first_start": sorted(round((b - first) / 1e5, 2) for _, b in st),
         }
     # 2: the collective is in flight when the fused kernel is launched
     for rep in range(2):
@@ -107,7 +122,7 @@ def main():
         res[f"before_{rep}"] = {"fused_ms": (m[1] - m[0]) / 1e5, "copy_ms": (m[3] - m[2]) / 1e5,
                                 "fused_start_after_copy_start_ms": (m[0] - m[2]) / 1e5,
                                 "copy_end_after_fused_start_ms": (m[3] - m[0]) / 1e5}
-    print(json.dumps(res, indent=1))
+    return res
 
 
 if __name__ == "__main__":
