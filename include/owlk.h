@@ -100,6 +100,15 @@ int owlk_adaln_bwd(const void* dy, long lddy, const void* x, long ldx, const flo
 int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const void* g, long ldg, long tpf,
                   long T, int d, void* dy, long lddy, void* dg, long lddg, int dg_bf16, float* dbias_frames,
                   long ldr, void* stream);
+/* adaln_bwd then gate_bwd on the dx it forms, in one pass (the DiT block's MLP-branch AdaLN backward
+ * feeding the attention branch's gate, modulation.py:28-55): dx as owlk_adaln_bwd (ypre none), then
+ * dyg = bf16(dx * g[t/tpf]), dg[f] = sum_t dx*y, dbias_frames[f] = sum_t dyg (optional) -- bit for bit
+ * the two calls, without reading dx back. */
+int owlk_adaln_gate_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd,
+                        const void* scale, long ldm, long tpf, long T, int d, const void* dres, long ldres,
+                        void* dx, long lddx, void* dscale, void* dshift, long ldg, int mod_bf16,
+                        const void* y, long ldy, const void* g, long ldgg, void* dyg, long lddyg, void* dg,
+                        long lddg, int dg_bf16, float* dbias_frames, long ldr, void* stream);
 
 /* ---- QK RMSNorm + RoPE (attn.py:83-89, rope.py:43-51): qkv rows [q(h d)|k(h d)|v(h d)] ->
  *   out rows [rope(bf16(rms(q)))|rope(bf16(rms(k)))], rotation pairs (2i, 2i+1) written to

@@ -64,26 +64,54 @@ __global__ __launch_bounds__(256) void adaln_fwd_k(const bf16* __restrict__ x, l
 // ------------------------------------------------------------------ AdaLN backward
 // one workgroup per frame (tpf token rows); wave w takes rows w, w+4, ...; each lane keeps the
 // per-column partial sums of its chunks, combined across the 4 waves through LDS at the end.
-template <int MAXC>
-__global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, long lddy,
+// GATE: the gate backward of the block's attention branch on the dx rows just formed (gate_bwd_k's
+// products in its order: the same rows per wave, the same lane partials and LDS combine), so dx is
+// not read back: dyg = bf16(dx * g[frame]), dg[frame] = sum_t dx*y, dbf[frame] = sum_t dyg.
+struct GateBwdArgs {
+  const bf16* y;
+  long ldy;
+  const bf16* g;
+  long ldgg;
+  bf16* dyg;
+  long lddyg;
+  float* dg;
+  long lddg;
+  int dg_bf16;
+  float* dbf;
+  long ldr;
+};
+
+template <int MAXC, bool GATE = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void adaln_bwd_k(const bf16* __restrict__ dy, long lddy,
                                                    const bf16* __restrict__ x, long ldx,
                                                    const float* __restrict__ rstd,
                                                    const bf16* __restrict__ sc, long ldm, long tpf, int d,
                                                    const bf16* __restrict__ dres, long ldres,
                                                    bf16* __restrict__ dx, long lddx,
                                                    float* __restrict__ dsc, float* __restrict__ dsh, long ldg,
-                                                   const bf16* __restrict__ ypre, int mod_bf16) {
+                                                   const bf16* __restrict__ ypre, int mod_bf16, GateBwdArgs ga = {}) {
   extern __shared__ float red[];  // [4][2][d]
   const long f = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = d / 8;
   float pa[MAXC][8], pb[MAXC][8];
   float t1[MAXC][8];
+  // GATE: each lane's gate partials live in its wave's slice of the LDS buffer (only that lane
+  // touches them until the combine), registers stay below occupancy 2's 256
+  bf16x8 gv[GATE ? MAXC : 1];  // the frame's gate row, packed
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
     const int c = lane + 64 * i;
 #pragma unroll
     for (int e = 0; e < 8; ++e) pa[i][e] = pb[i][e] = 0.f;
+    if constexpr (GATE) {
+      if (c < nch) {
+        gv[i] = *(const bf16x8*)(ga.g + f * ga.ldgg + c * 8);
+        float4* q = (float4*)(red + (w * 2 + 0) * d + c * 8);
+        float4* b = (float4*)(red + (w * 2 + 1) * d + c * 8);
+        q[0] = q[1] = b[0] = b[1] = float4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
     if (c < nch) {
       float a[8];
       unpack8(*(const bf16x8*)(sc + f * ldm + c * 8), a);
@@ -120,7 +148,8 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
       cres[i] = nres[i];
     }
     if (t + 4 < tpf) load(t + 4);
-    float g[MAXC][8], xh[MAXC][8];
+    // g = dy * (1 + scale) and xh = x * rstd are formed twice (for the row's dot product, then for
+    // dx) instead of kept: the rows stay packed in registers
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXC; ++i) {
@@ -137,15 +166,15 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
             const float sg = sigmoid_f(yp[e]);
             dv[e] = rb(dv[e] * sg * (1.f + yp[e] * (1.f - sg)));
           }
+          cdy[i] = pack8(dv);  // exact: dv is bf16-rounded
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          xh[i][e] = xv[e] * r;
-          const float xn = rb(xh[i][e]);
+          const float xh = xv[e] * r;
+          const float xn = rb(xh);
           pa[i][e] += dv[e] * xn;
           pb[i][e] += dv[e];
-          g[i][e] = dv[e] * t1[i][e];
-          dot += g[i][e] * xh[i][e];
+          dot += (dv[e] * t1[i][e]) * xh;
         }
       }
     }
@@ -154,13 +183,56 @@ __global__ __launch_bounds__(256) void adaln_bwd_k(const bf16* __restrict__ dy, 
     for (int i = 0; i < MAXC; ++i) {
       const int c = lane + 64 * i;
       if (c < nch) {
-        float o[8], rs[8];
+        float o[8], rs[8], dv[8], xv[8];
+        unpack8(cdy[i], dv);
+        unpack8(cx[i], xv);
         if (dres) unpack8(cres[i], rs);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = r * (g[i][e] - xh[i][e] * dot) + (dres ? rs[e] : 0.f);
-        *(bf16x8*)(dx + row * lddx + c * 8) = pack8(o);
+        for (int e = 0; e < 8; ++e) o[e] = r * (dv[e] * t1[i][e] - (xv[e] * r) * dot) + (dres ? rs[e] : 0.f);
+        const bf16x8 ov = pack8(o);
+        *(bf16x8*)(dx + row * lddx + c * 8) = ov;
+        if constexpr (GATE) {
+          float dv[8], yv[8], og[8], gf[8], qg[8], qb[8];
+          unpack8(ov, dv);
+          unpack8(*(const bf16x8*)(ga.y + row * ga.ldy + c * 8), yv);
+          unpack8(gv[i], gf);
+          float4* q = (float4*)(red + (w * 2 + 0) * d + c * 8);
+          float4* b = (float4*)(red + (w * 2 + 1) * d + c * 8);
+          *(float4*)qg = q[0];
+          *(float4*)(qg + 4) = q[1];
+          *(float4*)qb = b[0];
+          *(float4*)(qb + 4) = b[1];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            qg[e] += dv[e] * yv[e];
+            og[e] = rb(dv[e] * gf[e]);
+            qb[e] += og[e];
+          }
+          q[0] = *(float4*)qg;
+          q[1] = *(float4*)(qg + 4);
+          b[0] = *(float4*)qb;
+          b[1] = *(float4*)(qb + 4);
+          *(bf16x8*)(ga.dyg + row * ga.lddyg + c * 8) = pack8(og);
+        }
       }
     }
+  }
+  if constexpr (GATE) {  // the gate's partials: already in LDS, one slice per wave
+    __syncthreads();
+    for (int j = threadIdx.x; j < d; j += 256) {
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        sa += red[(ww * 2 + 0) * d + j];
+        sb += red[(ww * 2 + 1) * d + j];
+      }
+      if (ga.dg_bf16)
+        ((bf16*)ga.dg)[f * ga.lddg + j] = (bf16)sa;
+      else
+        ga.dg[f * ga.lddg + j] = sa;
+      if (ga.dbf) ga.dbf[f * ga.ldr + j] = sb;
+    }
+    __syncthreads();
   }
   // combine the 4 waves' column partials
 #pragma unroll
@@ -740,6 +812,36 @@ extern "C" int owlk_adaln_bwd(const void* dy, long lddy, const void* x, long ldx
                      (const bf16*)dres, ldres, (bf16*)dx, lddx, (float*)dscale, (float*)dshift, ldg, (const bf16*)ypre,
                      mod_bf16);
   return owlk::check_launch("adaln_bwd");
+}
+
+extern "C" int owlk_adaln_gate_bwd(const void* dy, long lddy, const void* x, long ldx, const float* rstd,
+                                   const void* scale, long ldm, long tpf, long T, int d, const void* dres, long ldres,
+                                   void* dx, long lddx, void* dscale, void* dshift, long ldg, int mod_bf16,
+                                   const void* y, long ldy, const void* g, long ldgg, void* dyg, long lddyg, void* dg,
+                                   long lddg, int dg_bf16, float* dbias_frames, long ldr, void* stream) {
+  OWLK_REQUIRE(d % 8 == 0 && d <= 64 * 8 * MAXCPL && tpf > 0 && T % tpf == 0,
+               "adaln_gate_bwd: bad d=%d tpf=%ld T=%ld", d, tpf, T);
+  OWLK_REQUIRE(y && g && dyg && dg, "adaln_gate_bwd: y, g, dyg and dg are required");
+  const GateBwdArgs ga{(const bf16*)y, ldy, (const bf16*)g, ldgg, (bf16*)dyg, lddyg, (float*)dg, lddg, dg_bf16,
+                       dbias_frames, ldr};
+  const dim3 grid((unsigned)(T / tpf));
+  const size_t lds = 8 * d * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+#define OWLK_AGB(C)                                                                                                  \
+  hipLaunchKernelGGL((adaln_bwd_k<C, true>), grid, dim3(256), lds, s, (const bf16*)dy, lddy, (const bf16*)x, ldx,    \
+                     rstd, (const bf16*)scale, ldm, tpf, d, (const bf16*)dres, ldres, (bf16*)dx, lddx, (float*)dscale, \
+                     (float*)dshift, ldg, (const bf16*)nullptr, mod_bf16, ga)
+  switch ((d / 8 + 63) / 64) {
+    case 1: OWLK_AGB(1); break;
+    case 2: OWLK_AGB(2); break;
+    case 3: OWLK_AGB(3); break;
+    case 4: OWLK_AGB(4); break;
+    case 5: OWLK_AGB(5); break;
+    case 6: OWLK_AGB(6); break;
+    default: OWLK_AGB(8); break;
+  }
+#undef OWLK_AGB
+  return owlk::check_launch("adaln_gate_bwd");
 }
 
 extern "C" int owlk_gate_bwd(const void* dout, long ldo, const void* y, long ldy, const void* g, long ldg, long tpf,

@@ -24,6 +24,8 @@ _SIGS = {
     "owlk_adaln_fwd": [P, L, P, P, L, L, L, I, P, L, P, P, P],
     "owlk_adaln_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, P, I, P],
     "owlk_gate_bwd": [P, L, P, L, P, L, L, L, I, P, L, P, L, I, P, L, P],
+    "owlk_adaln_gate_bwd": [P, L, P, L, P, P, L, L, L, I, P, L, P, L, P, P, L, I, P, L, P, L, P, L, P, L, I, P, L,
+                            P],
     "owlk_cond_embed": [P, I, P, I, F, P, L, P, I, L, P, I, F, P, P, L, P, P, I, L, I, I, P, L, L, P],
     "owlk_cond_silu_fwd": [P, P, P, P, L, L, I, P, P, P],
     "owlk_cond_silu_bwd": [P, I, P, P, L, L, I, P, P, P],

@@ -222,6 +222,30 @@ def adaln_bwd_into(dy, x, rstd, scale, tpf, dmod, dres=None, ypre=None):
     return dx
 
 
+# the DiT / MMDiT blocks' MLP-branch AdaLN backward with the attention gate's backward in one pass
+# (owlk_adaln_gate_bwd); OWLK_ADALN_GATE=0 runs the two passes (same bits), for A/B runs
+ADALN_GATE = os.environ.get("OWLK_ADALN_GATE", "1") != "0"
+
+
+def adaln_gate_bwd_into(dy, x, rstd, scale, tpf, dmod, dres, y, g, dg_out, want_bias=True):
+    """adaln_bwd_into followed by gate_bwd on its dx, in one pass (dx is not read back): ->
+    dx [T, d] bf16, the gate backward's dy [T, d] bf16, per-frame bias partials [F, d] fp32 (or None);
+    dg lands bf16 in dg_out.  Bit for bit the two separate calls."""
+    T, d = x.shape
+    F_ = T // tpf
+    assert dmod.dtype == BF16 and dmod.shape == (F_, 2 * d) and dmod.stride(1) == 1
+    assert dg_out.dtype == BF16 and dg_out.shape == (F_, d) and dg_out.stride(1) == 1
+    assert y.shape == (T, d) and y.stride(1) == 1 and g.shape == (F_, d) and g.stride(1) == 1
+    dx = torch.empty(T, d, device=x.device, dtype=BF16)
+    dyg = torch.empty(T, d, device=x.device, dtype=BF16)
+    dbf = torch.empty(F_, d, device=x.device, dtype=F32) if want_bias else None
+    call("owlk_adaln_gate_bwd", ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(rstd), ptr(scale), scale.stride(0),
+         tpf, T, d, ptr(dres), dres.stride(0) if dres is not None else 0, ptr(dx), d, ptr(dmod), ptr(dmod[:, d:]),
+         dmod.stride(0), 1, ptr(y), y.stride(0), ptr(g), g.stride(0), ptr(dyg), d, ptr(dg_out), dg_out.stride(0), 1,
+         ptr(dbf), d, stream())
+    return dx, dyg, dbf
+
+
 def gate_bwd(dout, y, g, tpf, want_bias=True, dg_out=None):
     """-> dy [T, d] bf16, dg [F, d] fp32 (or written as bf16 into dg_out, a [F, d] bf16 view of a
     modulation-gradient matrix), per-frame bias partials [F, d] fp32 (or None)."""

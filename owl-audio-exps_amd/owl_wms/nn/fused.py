@@ -412,11 +412,15 @@ class DiTBlockFn(torch.autograd.Function):
         del h2
         dh2 = K.gemm(dapre, bf16_weight(w1), b_trans=True)
         del dapre
-        dx1 = K.adaln_bwd_into(dh2, x1, r2, a2[:, :d], tpf, dm[:, 3 * d:5 * d], dres=dx2)
+        if K.ADALN_GATE:  # the attention branch's gate backward fused onto the dx rows (bit for bit)
+            dx1, dy1, dbf1 = K.adaln_gate_bwd_into(dh2, x1, r2, a2[:, :d], tpf, dm[:, 3 * d:5 * d], dx2, y1, gg1,
+                                                   dm[:, 2 * d:3 * d])
+        else:
+            dx1 = K.adaln_bwd_into(dh2, x1, r2, a2[:, :d], tpf, dm[:, 3 * d:5 * d], dres=dx2)
+            dy1, _, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf, dg_out=dm[:, 2 * d:3 * d])
         del dh2, x1
 
         # ---- attention branch
-        dy1, _, dbf1 = K.gate_bwd(dx1, y1, gg1, tpf, dg_out=dm[:, 2 * d:3 * d])
         dbout = bgrad_into(prm[3], dbf1)
         do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
         dwout = wgrad_into(prm[2], dy1, o)

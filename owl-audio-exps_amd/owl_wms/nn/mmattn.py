@@ -227,9 +227,13 @@ class MMDiTBlockFn(torch.autograd.Function):
                 wgrad(8 + 4 * s, dapre, h2)
                 dh2 = K.gemm(dapre, wts[s][1], b_trans=True)
                 del dapre, dy2
-                dx1 = K.adaln_bwd_into(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dm[:, 3 * d:5 * d], dres=douts[s])
+                if K.ADALN_GATE:  # + the attention output's gate backward on the dx rows (bit for bit)
+                    dx1, dy1, dbf1 = K.adaln_gate_bwd_into(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dm[:, 3 * d:5 * d],
+                                                           douts[s], y1, ms[:, 2 * d:3 * d], dm[:, 2 * d:3 * d])
+                else:
+                    dx1 = K.adaln_bwd_into(dh2, x1s, r2, ms[:, 3 * d:4 * d], ns[s], dm[:, 3 * d:5 * d], dres=douts[s])
+                    dy1, _, dbf1 = K.gate_bwd(dx1, y1, ms[:, 2 * d:3 * d], ns[s], dg_out=dm[:, 2 * d:3 * d])
                 # ---- attention output projection
-                dy1, _, dbf1 = K.gate_bwd(dx1, y1, ms[:, 2 * d:3 * d], ns[s], dg_out=dm[:, 2 * d:3 * d])
                 bgrad(5 + 2 * s, dbf1)
                 dos[s] = K.gemm(dy1, wts[s][2], b_trans=True, out=do_dst[s] if inplace else None)
                 wgrad(4 + 2 * s, dy1, os_[s])

@@ -1066,3 +1066,25 @@ def test_mlp_custom_unaligned_wide_input(k_in):
     for got, ref in ((x.grad, xr.grad), (m.fc1.weight.grad, w1.grad), (m.fc1.bias.grad, b1.grad),
                      (m.fc2.weight.grad, w2.grad), (m.fc2.bias.grad, b2.grad)):
         assert rel(got, ref) < 2e-2
+
+
+@pytest.mark.parametrize("d,tpf,F,bias", [(1536, 64, 6, True), (128, 1, 40, False), (2560, 65, 2, True),
+                                          (1536, 2, 9, True)])
+def test_adaln_gate_bwd_fused_equals_two_passes(d, tpf, F, bias):
+    """owlk_adaln_gate_bwd: the AdaLN backward and the gate backward on its dx in one pass, bit for bit
+    the two separate kernels (dx, dscale | dshift, the gated dy, dg, the bias partials)."""
+    k = K()
+    T = F * tpf
+    x = rnd(T, d, seed=40)
+    mod = rnd(F, 2 * d, scale=0.3, seed=41)
+    _, rstd = k.adaln_fwd(x, mod[:, :d], mod[:, d:], tpf)
+    dh, dres, y = rnd(T, d, seed=42), rnd(T, d, seed=43), rnd(T, d, seed=44)
+    g = rnd(F, d, seed=45)
+    dm0 = torch.zeros(F, 3 * d, device=DEV, dtype=torch.bfloat16)
+    dm1 = torch.zeros_like(dm0)
+    dx0 = k.adaln_bwd_into(dh, x, rstd, mod[:, :d], tpf, dm0[:, d:], dres=dres)
+    dy0, _, dbf0 = k.gate_bwd(dx0, y, g, tpf, want_bias=bias, dg_out=dm0[:, :d])
+    dx1, dy1, dbf1 = k.adaln_gate_bwd_into(dh, x, rstd, mod[:, :d], tpf, dm1[:, d:], dres, y, g, dm1[:, :d],
+                                           want_bias=bias)
+    assert torch.equal(dx0, dx1) and torch.equal(dy0, dy1) and torch.equal(dm0, dm1)
+    assert (dbf0 is None and dbf1 is None) or torch.equal(dbf0, dbf1)
