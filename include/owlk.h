@@ -70,6 +70,14 @@ int owlk_gemm_frames(long M, long N, long K, const void* A, long lda, long a_fs,
                      int c_f32, int epi, float alpha, float beta, const float* bias, void* aux, long ldaux,
                      const void* gate, long ldgate, long tpf, const void* resid, long ldres, void* ws,
                      long ws_bytes, void* stream);
+/* dO = dY W^T-layout product of the attention output projection's backward (attn.py:113: dY [M, K] bf16,
+ *   W [K, N] bf16 rows = the out-projection weight [out, in], bf16 dO [M, N]) AND the flash-attention
+ *   backward's delta[b, h, t] = sum_c dO[b L + t, h D + c] * O[b L + t, h D + c] (fp32 [M / L, H, L], as
+ *   owlk_attn_delta) in one launch when the shape takes the 256^2 ping-pong kernel at D = 64 (the
+ *   delta from the stored bf16 dO in owlk_attn_delta's order: the same bits); otherwise owlk_gemm +
+ *   owlk_attn_delta (then ldo must equal ldc).  N = H * D, M % L == 0. */
+int owlk_gemm_attn_delta(long M, long N, long K, const void* dY, long lddy, const void* W, long ldw, void* dO,
+                         long ldc, const void* o, long ldo, long L, int H, int D, float* delta, void* stream);
 /* bytes of split-K workspace owlk_gemm uses for these arguments (0: no split) */
 long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta);

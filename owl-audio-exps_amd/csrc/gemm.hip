@@ -26,6 +26,10 @@ enum Epi : int {
   EPI_DSILU = 3,       // C = bf16(bf16(acc) * silu'(aux)) (+ resid := bf16(silu(aux)))  (MLP fc1 bwd)
   EPI_AXPBY = 4,       // C = bf16(bf16(alpha*bf16(acc)) + bf16(beta*aux))        (Newton-Schulz)
   EPI_SCALE2 = 5,      // C = bf16(acc); aux = bf16(alpha*bf16(acc))   (NS: A = X X^T and c*A, muon.py:32-33)
+  // C = dO = bf16(alpha*acc) (the attention output's gradient, attn.py:113 backward) and the softmax
+  // backward's delta[b, h, t] = sum_c dO[r, 64 h + c] * O[r, 64 h + c] (r = b L + t, aux = O) from the
+  // stored bf16 values, attn_delta_k's products in its order: internal, owlk_gemm_attn_delta only
+  EPI_DELTA = 6,
 };
 
 constexpr int BK = 64;
@@ -53,6 +57,8 @@ struct GemmP {
   // -- the video rows of the MMDiT joint sequence (64 video + 1 audio token per frame, mmattn.py:54-60)
   // read / written in place; 0 = plain rows r * ld
   long a_fs, b_fs, c_fs;
+  float* delta;  // EPI_DELTA: [M / dl][N / 64][dl] fp32
+  long dl;
 };
 
 constexpr int FRAME_ROWS = 64;  // rows per frame of a frame-strided operand (OWLK_FRAME_ROWS)
@@ -432,6 +438,16 @@ DEV void epi_apply2(const GemmP& p, long c, long ao, long ro, float (&v)[8], con
     }
     st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, y));
     st_nt((bf16x8*)(p.aux + ao), __builtin_bit_cast(bf16x8, o));
+  } else if (EPI == EPI_DELTA) {
+    float sd = 0.f;  // this lane's 8 products O * dO, in attn_delta_k's order (the caller joins 8 lanes)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = cvt2(p.alpha * v[2 * k], p.alpha * v[2 * k + 1]);
+      sd += bf_lo(xw[k]) * bf_lo(o[k]);
+      sd += bf_hi(xw[k]) * bf_hi(o[k]);
+    }
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, o));
+    cs[0] = sd;
   }
 }
 
@@ -901,10 +917,11 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
       bb[e + 4] = rb(hi[e]);
     }
   }
-  constexpr bool HAS_X = EPI == EPI_GATE_RESID || EPI == EPI_DSILU || EPI == EPI_AXPBY;
+  constexpr bool HAS_X = EPI == EPI_GATE_RESID || EPI == EPI_DSILU || EPI == EPI_AXPBY || EPI == EPI_DELTA;
   constexpr bool HAS_G = EPI == EPI_GATE_RESID;
+  static_assert(EPI != EPI_DELTA || OWLK_GEMM_EPI2, "EPI_DELTA is built in the paired epilogue only");
   // prefetch depth (strips): every input of the tile up front where registers allow
-  constexpr int PD = (EPI == EPI_DSILU || EPI == EPI_AXPBY) ? 8 : (EPI == EPI_GATE_RESID ? 4 : 1);
+  constexpr int PD = (EPI == EPI_DSILU || EPI == EPI_AXPBY || EPI == EPI_DELTA) ? 8 : (EPI == EPI_GATE_RESID ? 4 : 1);
   bf16x8 xin[8][2], gin[8][2];  // [strip][q]
   // OWLK_GEMM_EPI2: per-lane element offsets of row wrow0 + (lane >> 3) in C / aux / resid; the row
   // chunks of the tile are wave-uniform steps d = 16 i + 8 q from them (frame-strided C: the chunk
@@ -984,8 +1001,18 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
           if (gm < p.M)
             epi_apply2<EPI, OF32>(p, cbase + c_step(d), abase + d * p.ldaux, rbase0 + d * p.ldres, v, bb, xin[i][q],
                                   gin[i][q], cs);
+          if constexpr (EPI == EPI_DELTA) {  // the row's 64 columns (one head) sit on 8 neighbouring lanes
+            float sd = gm < p.M ? cs[0] : 0.f;
+            sd += __shfl_xor(sd, 1, 64);
+            sd += __shfl_xor(sd, 2, 64);
+            sd += __shfl_xor(sd, 4, 64);
+            if ((lane & 7) == 0 && gm < p.M) {
+              const long b = gm / p.dl;
+              p.delta[(b * (p.N >> 6) + (gn >> 6)) * p.dl + (gm - b * p.dl)] = sd;
+            }
+          }
         } else if (gm < p.M) {
-          epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
+          if constexpr (EPI != EPI_DELTA) epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
         }
       }
     }
@@ -1103,10 +1130,14 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
     OWLK_REQUIRE(ok && pp, "gemm: frame-strided rows (mask %d) not built for this operand layout / epilogue", fs);
     return owlk::check_launch("gemm256");
   }
-  if (pp)
+  if constexpr (EPI == EPI_DELTA) {
+    OWLK_REQUIRE(pp && splits == 1 && batch == 1, "gemm: the delta epilogue runs in the unsplit ping-pong kernel");
     hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
-  else
+  } else if (pp) {
+    hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  } else {
     hipLaunchKernelGGL((gemm256_kernel<256, AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
+  }
   return owlk::check_launch("gemm256");
 }
 
@@ -1130,6 +1161,9 @@ int dispatch256(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStre
     case EPI_SCALE2:
       if (at || bt) break;
       return launch256<false, false, EPI_SCALE2, false>(p, batch, s);
+    case EPI_DELTA:  // the out-projection dX layout only: dO = dY W (W [out, in], k-contiguous rows of dY)
+      if (at || !bt) break;
+      return launch256<false, true, EPI_DELTA, false>(p, batch, s);
   }
   owlk::set_error("gemm: unknown epilogue %d", epi);
   return 1;
@@ -1666,6 +1700,36 @@ extern "C" int owlk_gemm(long M, long N, long K, long batch,
   if (colsum && !p.colsum)  // not fused by this kernel: a separate (workspace: deterministic) pass
     return owlk_colsum(C, 0, M, N, ldc, colsum, ws, ws_bytes, stream);
   return 0;
+}
+
+extern "C" int owlk_attn_delta(const void* o, const void* dout, long ld, long B, long L, int H, int D, float* delta,
+                               void* stream);
+
+// dO = dY W (bf16) and the attention backward's delta = rowsum(dO * O) per (sample, head, token): in the
+// ping-pong kernel's epilogue when the shape takes it (EPI_DELTA: the head's 64 columns are one wave's
+// strip columns, so dO is not read back), else the GEMM and owlk_attn_delta -- the same bits either way
+extern "C" int owlk_gemm_attn_delta(long M, long N, long K, const void* dY, long lddy, const void* W, long ldw,
+                                    void* dO, long ldc, const void* o, long ldo, long L, int H, int D,
+                                    float* delta, void* stream) {
+  OWLK_REQUIRE(L > 0 && M % L == 0 && H > 0 && D > 0 && N == (long)H * D && o && delta,
+               "gemm_attn_delta: bad shape M=%ld N=%ld L=%ld H=%d D=%d", M, N, L, H, D);
+  static const int pp = getenv("OWLK_GEMM_PP") ? atoi(getenv("OWLK_GEMM_PP")) : 1;
+  static const int fuse_env = getenv("OWLK_GEMM_DELTA") ? atoi(getenv("OWLK_GEMM_DELTA")) : 1;
+  const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256);
+  const SplitPlan pl = split_plan(M, N, K, 1, 0, 1, 0, EPI_DELTA, 0.f);
+  if (fuse_env && pp && D == 64 && fits256(M, N, K, 0, 1, 0, 0.f) && tiles256 >= min_tiles256() &&
+      pl.kind == SPLIT_NONE && ldo % 8 == 0 && (uintptr_t)o % 16 == 0) {
+    GemmP p{};
+    p.delta = delta;
+    p.dl = L;
+    return gemm_dispatch(p, M, N, K, 1, dY, lddy, 0, 0, W, ldw, 0, 1, dO, ldc, 0, 0, EPI_DELTA, 1.f, 0.f, nullptr,
+                         const_cast<void*>(o), ldo, 0, nullptr, 0, 0, 0, nullptr, 0, 0, nullptr, 0, stream);
+  }
+  OWLK_REQUIRE(ldo == ldc, "gemm_attn_delta: the unfused form needs O and dO with one row stride");
+  if (int e = owlk_gemm(M, N, K, 1, dY, lddy, 0, 0, W, ldw, 0, 1, dO, ldc, 0, 0, EPI_STORE, 1.f, 0.f, nullptr,
+                        nullptr, 0, 0, nullptr, 0, 0, 0, nullptr, 0, 0, nullptr, nullptr, 0, stream))
+    return e;
+  return owlk_attn_delta(o, dO, ldc, M / L, L, H, D, delta, stream);
 }
 
 extern "C" int owlk_gemm_frames(long M, long N, long K, const void* A, long lda, long a_fs, int a_trans,

@@ -52,6 +52,7 @@ _SIGS = {
     "owlk_attn_bwd_fused": [P, L, L, P, L, L, P, L, L, P, L, L, P, P, P, L, L, P, L, L, P, L, L, L, I, L, I, F, L, I, I,
                             P, P, P, P, L, P, L, I, P],
     "owlk_set_cu_reserve": [I],
+    "owlk_gemm_attn_delta": [L, L, L, P, L, P, L, P, L, P, L, L, I, I, P, P],
     "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
     "owlk_unpatchify": [P, I, I, L, P, P],
     "owlk_mse": [P, P, L, F, P, P, I, P, P],

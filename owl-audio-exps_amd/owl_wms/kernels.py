@@ -512,15 +512,35 @@ def attn_bwd_fused(q, k, v, do, lse, delta, H, D, mask, dq, dk, dv, scale, varia
     return ws
 
 
-def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None):
-    """Backward of attn_fwd (training shapes: Lq == Lkv, q_offset 0); all tensors [B, L, cols]."""
+def gemm_attn_delta(dy, w, o, H, D, L):
+    """dO = dy @ w (w: the out-projection weight [out, in], bf16) and delta [M / L, H, L] fp32 =
+    rowsum(dO * O) per head (the attention backward's softmax term) -> (dO [M, H D] bf16, delta);
+    one launch on the 256^2 ping-pong kernel's shapes (owlk_gemm_attn_delta)."""
+    M, K_ = dy.shape
+    N = w.shape[1]
+    assert w.shape[0] == K_ and N == H * D and M % L == 0 and o.shape == (M, N)
+    for t in (dy, w, o):
+        assert t.dtype == BF16 and t.stride(1) == 1
+    do = torch.empty(M, N, device=dy.device, dtype=BF16)
+    delta = torch.empty(M // L, H, L, device=dy.device, dtype=F32)
+    call("owlk_gemm_attn_delta", M, N, K_, ptr(dy), dy.stride(0), ptr(w), w.stride(0), ptr(do), N, ptr(o), o.stride(0),
+         L, H, D, ptr(delta), stream(), key="gemm_attn_delta", flops=2.0 * M * N * K_)
+    return do, delta
+
+
+def attn_bwd(q, k, v, o, do, lse, H, D, mask, dq, dk, dv, scale=None, delta=None):
+    """Backward of attn_fwd (training shapes: Lq == Lkv, q_offset 0); all tensors [B, L, cols].
+    delta: the softmax term rowsum(dO * O) [B, H, L] fp32 if the caller formed it (gemm_attn_delta)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do"), (dq, "dq"), (dk, "dk"), (dv, "dv")):
         _v3(t, n)
     B, L = q.shape[:2]
     scale = D ** -0.5 if scale is None else scale
-    delta = torch.empty(B, H, L, device=q.device, dtype=F32)
-    assert o.is_contiguous() and do.is_contiguous() and o.shape == do.shape
-    call("owlk_attn_delta", ptr(o), ptr(do), o.stride(1), B, L, H, D, ptr(delta), stream())
+    if delta is None:
+        delta = torch.empty(B, H, L, device=q.device, dtype=F32)
+        assert o.is_contiguous() and do.is_contiguous() and o.shape == do.shape
+        call("owlk_attn_delta", ptr(o), ptr(do), o.stride(1), B, L, H, D, ptr(delta), stream())
+    else:
+        assert delta.shape == (B, H, L) and delta.dtype == F32 and delta.is_contiguous()
     variant = fused_bwd_variant(D, mask)
     if variant is not None:
         # algorithmic FLOPs (SURVEY §8(d)): the backward's 8 D per allowed pair (dV, dP, dK, dQ)

@@ -422,7 +422,8 @@ class DiTBlockFn(torch.autograd.Function):
 
         # ---- attention branch
         dbout = bgrad_into(prm[3], dbf1)
-        do = K.gemm(dy1, bf16_weight(wout), b_trans=True)
+        # dO and the attention backward's delta = rowsum(dO * O) in one launch (the GEMM epilogue)
+        do, delta = K.gemm_attn_delta(dy1, bf16_weight(wout), o, H, D, T)
         dwout = wgrad_into(prm[2], dy1, o)
         del dy1
         if qkr is None:
@@ -432,8 +433,8 @@ class DiTBlockFn(torch.autograd.Function):
         q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
         dq3, dk3 = dqkr.view(B, T, 2 * d)[:, :, :d], dqkr.view(B, T, 2 * d)[:, :, d:]
         K.attn_bwd(q3, k3, qkv.view(B, T, 3 * d)[:, :, 2 * d:], o.view(B, T, d), do.view(B, T, d), lse, H, D,
-                   geo.mask, dq3, dk3, dqkv.view(B, T, 3 * d)[:, :, 2 * d:])
-        del do
+                   geo.mask, dq3, dk3, dqkv.view(B, T, 3 * d)[:, :, 2 * d:], delta=delta)
+        del do, delta
         # qkv bias gradient: the q / k columns' sums fused into the rope backward, the v columns' by colsum
         sink_bqkv = grad_sink(prm[1])
         dbqkv = sink_bqkv if sink_bqkv is not None else torch.zeros(3 * d, device=xx.device, dtype=torch.float32)

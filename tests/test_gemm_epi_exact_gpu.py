@@ -191,3 +191,26 @@ def test_split256_opt_plan_without_workspace():
         assert torch.equal(outs[0], outs[1])
         err = ((outs[0] - (ref + beta)).norm() / (ref + beta).norm()).item()
         assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("Mx,L", [(8232, 4116), (8192, 8192), (512, 256)])
+def test_gemm_attn_delta_equals_gemm_then_delta(Mx, L):
+    """owlk_gemm_attn_delta (the out-projection dX with the attention backward's delta in the ping-pong
+    epilogue, EPI_DELTA): dO bit for bit the plain GEMM and delta bit for bit owlk_attn_delta on that
+    dO -- ragged M (8,232 = 2 samples of 4,116 tokens, 198 tiles), one sample, and a shape below the
+    ping-pong minimum (512 x 1,536: the GEMM + attn_delta form)."""
+    from owl_wms import _lib
+    k = K()
+    H, D, Kd = 24, 64, 1536
+    g = torch.Generator().manual_seed(11)
+    dy = torch.randn(Mx, Kd, generator=g).bfloat16().to(DEV)
+    w = (torch.randn(Kd, H * D, generator=g) * 0.03).bfloat16().to(DEV)
+    o = torch.randn(Mx, H * D, generator=g).bfloat16().to(DEV)
+    do, delta = k.gemm_attn_delta(dy, w, o, H, D, L)
+    ref_do = k.gemm(dy, w, b_trans=True)
+    assert torch.equal(do, ref_do)
+    ref = torch.empty(Mx // L, H, L, device=DEV, dtype=torch.float32)
+    _lib.call("owlk_attn_delta", _lib.ptr(o), _lib.ptr(ref_do), H * D, Mx // L, L, H, D, _lib.ptr(ref), _lib.stream())
+    assert torch.equal(delta, ref)
+    exp = (do.float() * o.float()).view(Mx // L, L, H, D).sum(-1).transpose(1, 2)
+    assert ((delta - exp).abs().max() <= 1e-3 * exp.abs().max()).item()
