@@ -78,6 +78,13 @@ int owlk_gemm_frames(long M, long N, long K, const void* A, long lda, long a_fs,
  *   owlk_attn_delta (then ldo must equal ldc).  N = H * D, M % L == 0. */
 int owlk_gemm_attn_delta(long M, long N, long K, const void* dY, long lddy, const void* W, long ldw, void* dO,
                          long ldc, const void* o, long ldo, long L, int H, int D, float* delta, void* stream);
+/* qkv = A W^T + bias (the qkv projection, attn.py:82: A [M, K] bf16, W [N, K] bf16, N = 3 H D, bf16 qkv)
+ *   AND owlk_qk_rope_fwd of its q | k columns into out / rstd (same tables, positions and checks) in one
+ *   launch when the shape takes the 256^2 ping-pong kernel at D = 64 (the rotation from the stored bf16
+ *   qkv in qk_rope_fwd's order: the same bits); otherwise owlk_gemm + owlk_qk_rope_fwd. */
+int owlk_gemm_qk_rope(long M, long N, long K, const void* A, long lda, const void* W, long ldw, const float* bias,
+                      void* qkv, long ldq, int H, int D, const float* cosb, const float* sinb, long ld_tab, long n_tab,
+                      long tab_off, long tpos_div, void* out, long ldo, float* rstd, void* stream);
 /* bytes of split-K workspace owlk_gemm uses for these arguments (0: no split) */
 long owlk_gemm_splitk_bytes(long M, long N, long K, long batch, int a_trans, int b_trans, int c_f32, int epi,
                             float beta);

@@ -30,6 +30,10 @@ enum Epi : int {
   // backward's delta[b, h, t] = sum_c dO[r, 64 h + c] * O[r, 64 h + c] (r = b L + t, aux = O) from the
   // stored bf16 values, attn_delta_k's products in its order: internal, owlk_gemm_attn_delta only
   EPI_DELTA = 6,
+  // C = qkv = bf16(acc + bias) (attn.py:82) and, for the q | k columns, the QK-RMSNorm + RoPE rows
+  // (attn.py:83-89, rope.py:43-51) into aux = qkr [M, 2 H 64] with rstd [M, 2 H]: qk_rope_fwd_k's
+  // operations in its order on the stored bf16 values: internal, owlk_gemm_qk_rope only
+  EPI_QKROPE = 7,
 };
 
 constexpr int BK = 64;
@@ -59,7 +63,15 @@ struct GemmP {
   long a_fs, b_fs, c_fs;
   float* delta;  // EPI_DELTA: [M / dl][N / 64][dl] fp32
   long dl;
+  // EPI_QKROPE: rope tables [n_tab, 32] fp32 (row stride ld_tab) at row tab_off + (tpos_div ? r % tpos_div : r),
+  // rstd [M][qk_cols / 64]; the q | k columns are [0, qk_cols)
+  const float* rcos;
+  const float* rsin;
+  long ld_tab, tab_off, tpos_div;
+  float* rstd;
+  long qk_cols;
 };
+constexpr float QK_RMS_EPS = 1.1920928955078125e-07f;  // finfo(float32).eps, F.rms_norm default (elementwise.hip)
 
 constexpr int FRAME_ROWS = 64;  // rows per frame of a frame-strided operand (OWLK_FRAME_ROWS)
 #ifndef OWLK_GEMM_EPI2  // 1: gemm_pp_kernel's epilogue in paired-rounding form (epi_apply2); 0: epi_apply
@@ -438,6 +450,16 @@ DEV void epi_apply2(const GemmP& p, long c, long ao, long ro, float (&v)[8], con
     }
     st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, y));
     st_nt((bf16x8*)(p.aux + ao), __builtin_bit_cast(bf16x8, o));
+  } else if (EPI == EPI_QKROPE) {  // STORE (alpha 1, bias); the stored values go back to the caller in cs
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p.alpha * v[e] + bb[e];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = cvt2(v[2 * k], v[2 * k + 1]);
+      cs[2 * k] = bf_lo(o[k]);
+      cs[2 * k + 1] = bf_hi(o[k]);
+    }
+    st_nt((bf16x8*)((bf16*)p.C + c), __builtin_bit_cast(bf16x8, o));
   } else if (EPI == EPI_DELTA) {
     float sd = 0.f;  // this lane's 8 products O * dO, in attn_delta_k's order (the caller joins 8 lanes)
 #pragma unroll
@@ -919,7 +941,8 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
   }
   constexpr bool HAS_X = EPI == EPI_GATE_RESID || EPI == EPI_DSILU || EPI == EPI_AXPBY || EPI == EPI_DELTA;
   constexpr bool HAS_G = EPI == EPI_GATE_RESID;
-  static_assert(EPI != EPI_DELTA || OWLK_GEMM_EPI2, "EPI_DELTA is built in the paired epilogue only");
+  static_assert((EPI != EPI_DELTA && EPI != EPI_QKROPE) || OWLK_GEMM_EPI2,
+                "EPI_DELTA / EPI_QKROPE are built in the paired epilogue only");
   // prefetch depth (strips): every input of the tile up front where registers allow
   constexpr int PD = (EPI == EPI_DSILU || EPI == EPI_AXPBY || EPI == EPI_DELTA) ? 8 : (EPI == EPI_GATE_RESID ? 4 : 1);
   bf16x8 xin[8][2], gin[8][2];  // [strip][q]
@@ -1001,6 +1024,36 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
           if (gm < p.M)
             epi_apply2<EPI, OF32>(p, cbase + c_step(d), abase + d * p.ldaux, rbase0 + d * p.ldres, v, bb, xin[i][q],
                                   gin[i][q], cs);
+          if constexpr (EPI == EPI_QKROPE) {  // the row's 64 columns (one q / k head) on 8 neighbouring lanes
+            if (wcol0 < p.qk_cols) {
+              float ss = 0.f;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) ss += cs[e] * cs[e];
+              ss = gm < p.M ? ss : 0.f;
+              ss += __shfl_xor(ss, 1, 64);
+              ss += __shfl_xor(ss, 2, 64);
+              ss += __shfl_xor(ss, 4, 64);
+              const float r = rsqrtf(ss / 64 + QK_RMS_EPS);
+              if (gm < p.M) {
+                const int j = lane & 7;
+                const long wh = wcol0 >> 6;
+                if (j == 0 && p.rstd) p.rstd[gm * (p.qk_cols >> 6) + wh] = r;
+                const long pos = p.tab_off + (p.tpos_div > 0 ? gm % p.tpos_div : gm);
+                const f32x4 cv = *(const f32x4*)(p.rcos + pos * p.ld_tab + j * 4);
+                const f32x4 sv = *(const f32x4*)(p.rsin + pos * p.ld_tab + j * 4);
+                bf16x4 y0, y1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float x0 = rb(cs[2 * e] * r), x1 = rb(cs[2 * e + 1] * r);
+                  y0[e] = (bf16)(x0 * cv[e] - x1 * sv[e]);
+                  y1[e] = (bf16)(x1 * cv[e] + x0 * sv[e]);
+                }
+                bf16* ro = p.aux + gm * p.ldaux + wh * 64;
+                *(bf16x4*)(ro + j * 4) = y0;
+                *(bf16x4*)(ro + 32 + j * 4) = y1;
+              }
+            }
+          }
           if constexpr (EPI == EPI_DELTA) {  // the row's 64 columns (one head) sit on 8 neighbouring lanes
             float sd = gm < p.M ? cs[0] : 0.f;
             sd += __shfl_xor(sd, 1, 64);
@@ -1012,7 +1065,8 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
             }
           }
         } else if (gm < p.M) {
-          if constexpr (EPI != EPI_DELTA) epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
+          if constexpr (EPI != EPI_DELTA && EPI != EPI_QKROPE)
+            epi_apply<EPI, OF32, FC>(p, z, gm, gn, v, bb, xin[i][q], gin[i][q], cs);
         }
       }
     }
@@ -1130,8 +1184,8 @@ int launch256(GemmP& p, long batch, hipStream_t s) {
     OWLK_REQUIRE(ok && pp, "gemm: frame-strided rows (mask %d) not built for this operand layout / epilogue", fs);
     return owlk::check_launch("gemm256");
   }
-  if constexpr (EPI == EPI_DELTA) {
-    OWLK_REQUIRE(pp && splits == 1 && batch == 1, "gemm: the delta epilogue runs in the unsplit ping-pong kernel");
+  if constexpr (EPI == EPI_DELTA || EPI == EPI_QKROPE) {
+    OWLK_REQUIRE(pp && splits == 1 && batch == 1, "gemm: the delta / rope epilogues run in the unsplit ping-pong kernel");
     hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
   } else if (pp) {
     hipLaunchKernelGGL((gemm_pp_kernel<AT, BT, EPI, OF32>), grid, dim3(NT8), 0, s, p);
@@ -1164,6 +1218,9 @@ int dispatch256(GemmP& p, int at, int bt, int epi, int cf32, long batch, hipStre
     case EPI_DELTA:  // the out-projection dX layout only: dO = dY W (W [out, in], k-contiguous rows of dY)
       if (at || !bt) break;
       return launch256<false, true, EPI_DELTA, false>(p, batch, s);
+    case EPI_QKROPE:  // the qkv projection's layout only: qkv = h W^T + b
+      if (at || bt) break;
+      return launch256<false, false, EPI_QKROPE, false>(p, batch, s);
   }
   owlk::set_error("gemm: unknown epilogue %d", epi);
   return 1;
@@ -1730,6 +1787,48 @@ extern "C" int owlk_gemm_attn_delta(long M, long N, long K, const void* dY, long
                         nullptr, 0, 0, nullptr, 0, 0, 0, nullptr, 0, 0, nullptr, nullptr, 0, stream))
     return e;
   return owlk_attn_delta(o, dO, ldc, M / L, L, H, D, delta, stream);
+}
+
+extern "C" int owlk_qk_rope_fwd(const void* qkv, long ldq, long T, int H, int D, const float* cosb,
+                                const float* sinb, long ld_tab, long n_tab, long tab_off, long tpos_div, void* out,
+                                long ldo, float* rstd, void* stream);
+
+// qkv = h W^T + b (bf16) and the QK-RMSNorm + RoPE rows of its q | k columns: in the ping-pong kernel's
+// epilogue when the shape takes it (EPI_QKROPE: a head's 64 columns are one wave's strip columns, so
+// qkv is not read back), else the GEMM and owlk_qk_rope_fwd -- the same bits either way
+extern "C" int owlk_gemm_qk_rope(long M, long N, long K, const void* A, long lda, const void* W, long ldw,
+                                 const float* bias, void* qkv, long ldq, int H, int D, const float* cosb,
+                                 const float* sinb, long ld_tab, long n_tab, long tab_off, long tpos_div, void* out,
+                                 long ldo, float* rstd, void* stream) {
+  OWLK_REQUIRE(H > 0 && (D == 64 || D == 128) && N == 3L * H * D && out && cosb && sinb,
+               "gemm_qk_rope: bad shape N=%ld H=%d D=%d", N, H, D);
+  {
+    const long span = tpos_div > 0 ? (M < tpos_div ? M : tpos_div) : M;
+    OWLK_REQUIRE(n_tab > 0 && tab_off >= 0 && tab_off + span <= n_tab,
+                 "gemm_qk_rope: positions %ld.. past the %ld-row rope table", tab_off, n_tab);
+  }
+  static const int pp = getenv("OWLK_GEMM_PP") ? atoi(getenv("OWLK_GEMM_PP")) : 1;
+  static const int fuse_env = getenv("OWLK_GEMM_ROPE") ? atoi(getenv("OWLK_GEMM_ROPE")) : 1;
+  const long tiles256 = ((M + 255) / 256) * ((N + 255) / 256);
+  const SplitPlan pl = split_plan(M, N, K, 1, 0, 0, 0, EPI_QKROPE, 0.f);
+  if (fuse_env && pp && D == 64 && fits256(M, N, K, 0, 0, 0, 0.f) && tiles256 >= min_tiles256() &&
+      pl.kind == SPLIT_NONE && ldo % 8 == 0 && ld_tab % 4 == 0 && (uintptr_t)out % 16 == 0 &&
+      (uintptr_t)cosb % 16 == 0 && (uintptr_t)sinb % 16 == 0) {
+    GemmP p{};
+    p.rcos = cosb;
+    p.rsin = sinb;
+    p.ld_tab = ld_tab;
+    p.tab_off = tab_off;
+    p.tpos_div = tpos_div;
+    p.rstd = rstd;
+    p.qk_cols = 2L * H * D;
+    return gemm_dispatch(p, M, N, K, 1, A, lda, 0, 0, W, ldw, 0, 0, qkv, ldq, 0, 0, EPI_QKROPE, 1.f, 0.f, bias, out,
+                         ldo, 0, nullptr, 0, 0, 0, nullptr, 0, 0, nullptr, 0, stream);
+  }
+  if (int e = owlk_gemm(M, N, K, 1, A, lda, 0, 0, W, ldw, 0, 0, qkv, ldq, 0, 0, EPI_STORE, 1.f, 0.f, bias, nullptr,
+                        0, 0, nullptr, 0, 0, 0, nullptr, 0, 0, nullptr, nullptr, 0, stream))
+    return e;
+  return owlk_qk_rope_fwd(qkv, ldq, M, H, D, cosb, sinb, ld_tab, n_tab, tab_off, tpos_div, out, ldo, rstd, stream);
 }
 
 extern "C" int owlk_gemm_frames(long M, long N, long K, const void* A, long lda, long a_fs, int a_trans,

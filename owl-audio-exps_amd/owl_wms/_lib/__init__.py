@@ -53,6 +53,7 @@ _SIGS = {
                             P, P, P, P, L, P, L, I, P],
     "owlk_set_cu_reserve": [I],
     "owlk_gemm_attn_delta": [L, L, L, P, L, P, L, P, L, P, L, L, I, I, P, P],
+    "owlk_gemm_qk_rope": [L, L, L, P, L, P, L, P, P, L, I, I, P, P, L, L, L, L, P, L, P, P],
     "owlk_flow_noise": [P, P, P, I, I, L, P, P, P, P],
     "owlk_unpatchify": [P, I, I, L, P, P],
     "owlk_mse": [P, P, L, F, P, P, I, P, P],

@@ -285,6 +285,23 @@ def qk_rope_fwd(qkv, H, D, cos, sin, tab_off=0, tpos_div=0):
     return out, rstd
 
 
+def gemm_qk_rope(h, w, bias, H, D, cos, sin, tab_off=0, tpos_div=0):
+    """qkv = h @ w^T + bias [M, 3 H D] bf16 and qk_rope_fwd(qkv, ...) -> (qkv, out, rstd); one launch on
+    the 256^2 ping-pong kernel's shapes (owlk_gemm_qk_rope), the same bits as the two calls."""
+    M, K_ = h.shape
+    N = w.shape[0]
+    assert w.shape[1] == K_ and N == 3 * H * D and h.dtype == BF16 and w.dtype == BF16
+    assert h.stride(1) == 1 and w.stride(1) == 1 and cos.stride(1) == 1 and sin.stride(0) == cos.stride(0)
+    assert bias is None or (bias.dtype == F32 and bias.is_contiguous())
+    qkv = torch.empty(M, N, device=h.device, dtype=BF16)
+    out = torch.empty(M, 2 * H * D, device=h.device, dtype=BF16)
+    rstd = torch.empty(M, 2 * H, device=h.device, dtype=F32)
+    call("owlk_gemm_qk_rope", M, N, K_, ptr(h), h.stride(0), ptr(w), w.stride(0), ptr(bias), ptr(qkv), N, H, D,
+         ptr(cos), ptr(sin), cos.stride(0), cos.shape[0], tab_off, tpos_div, ptr(out), out.stride(0), ptr(rstd),
+         stream(), key="gemm_qk_rope", flops=2.0 * M * N * K_)
+    return qkv, out, rstd
+
+
 def qk_rope_fwd_kv(qkv, B, L, H, D, cos, sin, tab_off, q_out, k_out, v_out):
     """Decode form: qkv [B L, 3 H D] -> rotated q into q_out [B, L, H D], rotated k into k_out and
     v copied into v_out (views of the KV cache's slots; any row / batch strides)."""

@@ -342,8 +342,8 @@ class DiTBlockFn(torch.autograd.Function):
         a1, gg1, a2, gg2 = mods[:, :2 * d], mods[:, 2 * d:3 * d], mods[:, 3 * d:5 * d], mods[:, 5 * d:]
 
         h1, r1 = K.adaln_fwd(xx, a1[:, :d], a1[:, d:], tpf)
-        qkv = K.gemm(h1, bf16_weight(wqkv), bias=bqkv)
-        qkr, rq = K.qk_rope_fwd(qkv, H, D, geo.cos, geo.sin, geo.tab_off, T)
+        # qkv and its QK-RMSNorm + RoPE rows in one launch (the GEMM epilogue)
+        qkv, qkr, rq = K.gemm_qk_rope(h1, bf16_weight(wqkv), bqkv, H, D, geo.cos, geo.sin, geo.tab_off, T)
         q3, k3 = qkr.view(B, T, 2 * d)[:, :, :d], qkr.view(B, T, 2 * d)[:, :, d:]
         kept = _kept_attention(geo, x, wqkv)
         if kept is not None:

@@ -214,3 +214,25 @@ def test_gemm_attn_delta_equals_gemm_then_delta(Mx, L):
     assert torch.equal(delta, ref)
     exp = (do.float() * o.float()).view(Mx // L, L, H, D).sum(-1).transpose(1, 2)
     assert ((delta - exp).abs().max() <= 1e-3 * exp.abs().max()).item()
+
+
+@pytest.mark.parametrize("Mx,tpos,off", [(8232, 4116, 0), (8192, 0, 3), (512, 256, 0)])
+def test_gemm_qk_rope_equals_gemm_then_rope(Mx, tpos, off):
+    """owlk_gemm_qk_rope (the qkv projection with QK-RMSNorm + RoPE in the ping-pong epilogue,
+    EPI_QKROPE): qkv bit for bit the plain GEMM + bias, the rotated q | k rows and rstd bit for bit
+    owlk_qk_rope_fwd on that qkv -- ragged M with per-sample positions, one sample with a table
+    offset, and a shape below the ping-pong minimum (the GEMM + qk_rope_fwd form)."""
+    k = K()
+    from oracle import ref_ops as R
+    H, D, Kd = 8, 64, 1536
+    g = torch.Generator().manual_seed(12)
+    h = torch.randn(Mx, Kd, generator=g).bfloat16().to(DEV)
+    w = (torch.randn(3 * H * D, Kd, generator=g) * 0.03).bfloat16().to(DEV)
+    bias = torch.randn(3 * H * D, generator=g).float().to(DEV)
+    ang = R.motion_rope_angles(Mx // 64 + 8, 8, D)
+    cos, sin = ang.cos().to(DEV).contiguous(), ang.sin().to(DEV).contiguous()
+    qkv, out, rstd = k.gemm_qk_rope(h, w, bias, H, D, cos, sin, off, tpos)
+    ref_qkv = k.gemm(h, w, bias=bias)
+    assert torch.equal(qkv, ref_qkv)
+    ref_out, ref_rstd = k.qk_rope_fwd(ref_qkv, H, D, cos, sin, off, tpos)
+    assert torch.equal(out, ref_out) and torch.equal(rstd, ref_rstd)
