@@ -158,6 +158,10 @@ class DiTBlock(nn.Module):
         self.adaln2 = AdaLN(dim)
         self.gate2 = Gate(dim)
         self.config = config
+        # GradReducer lays these four weights' gradient views out back to back in this order, a [6d, d]
+        # stack: the block's backward then forms their gradients as ONE weight-gradient GEMM
+        for i, w in enumerate(self.mod_params()[0]):
+            w._owl_grad_stack = (id(self), i)
 
     def modulation(self, cond):
         """(adaln1 [2d], gate1 [d], adaln2 [2d], gate2 [d]) per frame from silu(cond): one stacked GEMM

@@ -27,6 +27,7 @@ reducer is told the gradient is complete.  That replaces autograd's separate fp3
 ``p.grad += g`` pass per parameter per micro-step.  It needs each parameter used once per
 forward, which holds for every module on this path.
 """
+import os
 import weakref
 
 import torch
@@ -457,13 +458,40 @@ class DiTBlockFn(torch.autograd.Function):
         # ---- modulation: one dX GEMM against the stack onto the CondGrad of s; dW / db per fc
         ds = cond_grad_add(ctx.cg, dm, wmod, ctx.sshape) if ctx.needs_input_grad[1] else None
         mgrads = []
+        stacked = _stacked_mod_sink([prm[8 + 2 * i] for i in range(4)], d) \
+            if all(ctx.needs_input_grad[13 + 2 * i] for i in range(4)) else None
+        if stacked is not None:  # the four weights' gradient views are one [6d, d] stack: ONE GEMM
+            K.gemm(dm, s2, a_trans=True, b_trans=True, out=stacked, out_f32=True, beta=1.0)
         for i, (lo, hi) in enumerate(_MOD_COLS(d)):
             w, bias = prm[8 + 2 * i], prm[9 + 2 * i]
             dmi = dm[:, lo:hi]
-            mgrads.append(wgrad_into(w, dmi, s2) if ctx.needs_input_grad[13 + 2 * i] else None)
+            if stacked is not None:
+                grad_done(w)
+                mgrads.append(None)
+            else:
+                mgrads.append(wgrad_into(w, dmi, s2) if ctx.needs_input_grad[13 + 2 * i] else None)
             mgrads.append(bgrad_into(bias, dmi) if ctx.needs_input_grad[14 + 2 * i] else None)
         return (dx.view(B, T, d), ds, None, None, None,
                 dwqkv, dbqkv, dwout, dbout, dw1, db1, dw2, db2, *mgrads)
+
+
+_MOD_STACK_GEMM = os.environ.get("OWL_MOD_STACK_GEMM", "1") != "0"  # 0: four weight-gradient GEMMs (A/B)
+
+
+def _stacked_mod_sink(ws, d):
+    """[6d, d] fp32 view over the four modulation weights' bucket views when GradReducer laid them
+    out back to back in column order (DiTBlock tags them, utils/grad_reducer.py), else None."""
+    if not _MOD_STACK_GEMM:
+        return None
+    sinks = [grad_sink(w) for w in ws]
+    if any(v is None or not v.is_contiguous() for v in sinks):
+        return None
+    off = 0
+    for v, (lo, hi) in zip(sinks, _MOD_COLS(d)):
+        if v.shape != (hi - lo, d) or v.data_ptr() != sinks[0].data_ptr() + off * 4:
+            return None
+        off += v.numel()
+    return torch.as_strided(sinks[0], (6 * d, d), (d, 1))
 
 
 def _MOD_COLS(d):

@@ -30,13 +30,27 @@ class GradReducer:
         self.ws = world_size if world_size is not None else (dist.get_world_size() if dist.is_initialized() else 1)
         cap = bucket_mb * (1 << 20) // 4
         self.buckets = []  # list of (flat buffer, [params])
+        # parameters tagged _owl_grad_stack = (group, index) get their views back to back in index
+        # order, in one bucket (the DiT block's four modulation weights: one [6d, d] weight-gradient GEMM)
+        stacks = {}
+        for p in self.params:
+            tag = getattr(p, "_owl_grad_stack", None)
+            if tag is not None:
+                stacks.setdefault(tag[0], []).append((tag[1], p))
+        placed = set()
         cur, cur_n = [], 0
         for p in reversed(self.params):
-            if cur and cur_n + p.numel() > cap:
+            if id(p) in placed:
+                continue
+            tag = getattr(p, "_owl_grad_stack", None)
+            unit = [q for _, q in sorted(stacks[tag[0]], key=lambda t: t[0])] if tag is not None else [p]
+            n = sum(q.numel() for q in unit)
+            if cur and cur_n + n > cap:
                 self.buckets.append(cur)
                 cur, cur_n = [], 0
-            cur.append(p)
-            cur_n += p.numel()
+            cur.extend(unit)
+            cur_n += n
+            placed.update(id(q) for q in unit)
         if cur:
             self.buckets.append(cur)
         self.flat = []

@@ -566,3 +566,31 @@ def test_batch_permute_to_length():
     m2, b2 = batch_permute_to_length(m, b, 17)
     assert m2.shape == (4, 17, 2) and b2.shape == (4, 17, 11)
     assert torch.equal(m2[:, :5], m) and torch.equal(b2[:, :5], b)
+
+
+def test_grad_reducer_stacks_tagged_params_back_to_back():
+    """Parameters tagged _owl_grad_stack (the DiT block's four modulation weights) get adjacent bucket
+    views in index order, whatever the bucket size, so the block's backward can form their gradients
+    as one [6d, d] GEMM (nn/fused.py _stacked_mod_sink)."""
+    from owl_wms.configs import model_config
+    from owl_wms.models.gamerft import GameRFT
+    from owl_wms.nn.fused import _stacked_mod_sink
+    from owl_wms.utils.grad_reducer import GradReducer
+    cfg = model_config(model_id="game_rft", sample_size=8, channels=32, n_layers=2, n_heads=2, d_model=128,
+                       tokens_per_frame=64, n_buttons=11, cfg_prob=0.1, n_frames=8, causal=True, uncond=False,
+                       backbone="dit", has_audio=False, rope_impl="motion", local_window=2, global_window=None)
+    m = GameRFT(cfg)
+    for mb in (256, 0.05):  # one bucket; buckets smaller than a stack (the stack stays whole)
+        red = GradReducer(m.parameters(), bucket_mb=mb, world_size=1)
+        blocks = [b for b in m.modules() if hasattr(b, "mod_params") and hasattr(b, "gate2")]
+        assert blocks
+        for b in blocks:
+            ws = b.mod_params()[0]
+            assert len({red.bucket_of[w] for w in ws}) == 1
+            st = _stacked_mod_sink(ws, 128)
+            assert st is not None and st.shape == (6 * 128, 128)
+            st.fill_(0)
+            st[:256].fill_(1)
+            assert (ws[0].grad == 1).all() and (ws[1].grad == 0).all()
+        for h in red.hooks:
+            h.remove()
