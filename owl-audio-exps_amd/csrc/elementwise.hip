@@ -82,7 +82,7 @@ struct GateBwdArgs {
 };
 
 template <int MAXC, bool GATE = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void adaln_bwd_k(const bf16* __restrict__ dy, long lddy,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXC <= 3 ? 2 : 1))) void adaln_bwd_k(const bf16* __restrict__ dy, long lddy,
                                                    const bf16* __restrict__ x, long ldx,
                                                    const float* __restrict__ rstd,
                                                    const bf16* __restrict__ sc, long ldm, long tpf, int d,
