@@ -983,6 +983,21 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (!atomic && i + PD < 8) load_in(i + PD, xin[i + PD], gin[i + PD]);
+    // EPI_QKROPE: this strip's rope table rows, loaded before the strip is staged through LDS so their
+    // latency hides behind it (the rotation of row chunk q reads rcv[q] / rsv[q])
+    f32x4 rcv[2], rsv[2];
+    if constexpr (EPI == EPI_QKROPE) {
+      if (wcol0 < p.qk_cols) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          long gm = wrow0 + 16 * i + 8 * q + (lane >> 3);
+          gm = gm < p.M ? gm : p.M - 1;
+          const long pos = p.tab_off + (p.tpos_div > 0 ? gm % p.tpos_div : gm);
+          rcv[q] = *(const f32x4*)(p.rcos + pos * p.ld_tab + (lane & 7) * 4);
+          rsv[q] = *(const f32x4*)(p.rsin + pos * p.ld_tab + (lane & 7) * 4);
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1038,9 +1053,7 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
                 const int j = lane & 7;
                 const long wh = wcol0 >> 6;
                 if (j == 0 && p.rstd) p.rstd[gm * (p.qk_cols >> 6) + wh] = r;
-                const long pos = p.tab_off + (p.tpos_div > 0 ? gm % p.tpos_div : gm);
-                const f32x4 cv = *(const f32x4*)(p.rcos + pos * p.ld_tab + j * 4);
-                const f32x4 sv = *(const f32x4*)(p.rsin + pos * p.ld_tab + j * 4);
+                const f32x4 cv = rcv[q], sv = rsv[q];
                 bf16x4 y0, y1;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
