@@ -148,6 +148,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXC <= 3 ?
       cres[i] = nres[i];
     }
     if (t + 4 < tpf) load(t + 4);
+    bf16x8 cyg[GATE ? MAXC : 1];  // GATE: this row of y, loaded now so its latency hides behind the reduction
+    if constexpr (GATE) {
+#pragma unroll
+      for (int i = 0; i < MAXC; ++i)
+        if (lane + 64 * i < nch) cyg[i] = *(const bf16x8*)(ga.y + row * ga.ldy + (lane + 64 * i) * 8);
+    }
     // g = dy * (1 + scale) and xh = x * rstd are formed twice (for the row's dot product, then for
     // dx) instead of kept: the rows stay packed in registers
     float dot = 0.f;
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MAXC <= 3 ?
         if constexpr (GATE) {
           float dv[8], yv[8], og[8], gf[8], qg[8], qb[8];
           unpack8(ov, dv);
-          unpack8(*(const bf16x8*)(ga.y + row * ga.ldy + c * 8), yv);
+          unpack8(cyg[i], yv);
           unpack8(gv[i], gf);
           float4* q = (float4*)(red + (w * 2 + 0) * d + c * 8);
           float4* b = (float4*)(red + (w * 2 + 1) * d + c * 8);
