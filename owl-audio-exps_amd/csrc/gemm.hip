@@ -1061,9 +1061,14 @@ __global__ __launch_bounds__(NT8, 1) void gemm_pp_kernel(GemmP p) {
                   y0[e] = (bf16)(x0 * cv[e] - x1 * sv[e]);
                   y1[e] = (bf16)(x1 * cv[e] + x0 * sv[e]);
                 }
-                bf16* ro = p.aux + gm * p.ldaux + wh * 64;
-                *(bf16x4*)(ro + j * 4) = y0;
-                *(bf16x4*)(ro + 32 + j * 4) = y1;
+                // lane pairs (j, j ^ 1) share the row: swap halves so each lane stores 16 B, the even lane
+                // both y0 quads (q positions 8 m .. 8 m + 7), the odd lane both y1 quads (32 + 8 m ..)
+                const uint2 w0 = __builtin_bit_cast(uint2, y0), w1 = __builtin_bit_cast(uint2, y1);
+                const bool odd = j & 1;
+                const uint2 snd = odd ? w0 : w1;
+                const uint2 rcv{(unsigned)__shfl_xor((int)snd.x, 1, 64), (unsigned)__shfl_xor((int)snd.y, 1, 64)};
+                const u32x4 ow = odd ? u32x4{rcv.x, rcv.y, w1.x, w1.y} : u32x4{w0.x, w0.y, rcv.x, rcv.y};
+                *(u32x4*)(p.aux + gm * p.ldaux + wh * 64 + (odd ? 32 : 0) + 8 * (j >> 1)) = ow;
               }
             }
           }
